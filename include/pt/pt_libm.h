@@ -1,0 +1,112 @@
+/*
+ * pt_libm.h — a tiny deterministic libm (sinf / cosf / sincosf / pow(x, 5)) that gives the
+ * SAME bits on the x86 host (gcc / g++) and on gfx950 (hipcc device code).
+ *
+ * Why it exists: the reference's BSDFs call sinf/cosf/powf (interactions.cu:74-75, 201, 253,
+ * 260; pathtrace.cu:236).  The reference binary used CUDA libdevice; a host restatement uses
+ * glibc; HIP device code would use ocml.  All three differ in the last ulp, and a Monte-Carlo
+ * path is chaotic, so a 1-ulp difference re-routes a path.  Both the oracle (in its
+ * "portable" trig mode) and the HIP kernels call these functions, so oracle-vs-GPU parity
+ * can be checked BIT-EXACTLY; the oracle's "libm" mode (glibc) is what is compared with the
+ * reference-derived known answers, within the statistical tolerance of SURVEY §8c.
+ *
+ * Method: promote the float argument to double, Cody–Waite reduce by pi/2 with a 3-part
+ * constant (fdlibm's pio2_1/2/3), evaluate fdlibm's __kernel_sin / __kernel_cos minimax
+ * polynomials (public-domain coefficients), round once to float.  Every operation is a plain
+ * IEEE double op; callers MUST compile with -ffp-contract=off so no FMA is formed on either
+ * side.  Result error is < 0.5 ulp + 2^-40 relative, i.e. correctly rounded except in
+ * vanishingly rare near-halfway cases — identically on both sides.
+ *
+ * This is test/product shared *libm*, not part of the reference algorithm.
+ */
+#ifndef PT_LIBM_H
+#define PT_LIBM_H
+
+#if defined(__HIPCC__)
+#define PT_LIBM_FN __host__ __device__ static inline
+#else
+#define PT_LIBM_FN static inline
+#endif
+
+PT_LIBM_FN double pt_libm_floor(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_floor(x);
+#else
+    return __builtin_floor(x);
+#endif
+}
+
+PT_LIBM_FN double pt_kernel_sin(double x) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x;
+    double p = S5 + z * S6;
+    p = S4 + z * p;
+    p = S3 + z * p;
+    p = S2 + z * p;
+    p = S1 + z * p;
+    return x + (x * z) * p;
+}
+
+PT_LIBM_FN double pt_kernel_cos(double x) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x;
+    double p = C5 + z * C6;
+    p = C4 + z * p;
+    p = C3 + z * p;
+    p = C2 + z * p;
+    p = C1 + z * p;
+    return (1.0 - 0.5 * z) + (z * z) * p;
+}
+
+/* sin and cos of a float, each rounded once to float. */
+PT_LIBM_FN void pt_sincosf(float xf, float* s_out, float* c_out) {
+    double x = (double)xf;
+    double ax = x < 0.0 ? -x : x;
+    if (!(ax < 1.0e9)) {            /* inf / NaN / absurdly large: NaN like libm for inf/NaN */
+        float nan = xf - xf;
+        if (ax == ax && ax >= 1.0e9) nan = 0.0f / 0.0f;
+        *s_out = nan;
+        *c_out = nan;
+        return;
+    }
+    const double INV_PIO2 = 6.36619772367581382433e-01;
+    const double PIO2_1 = 1.57079632673412561417e+00;   /* first 33 bits of pi/2 */
+    const double PIO2_2 = 6.07710050630396597660e-11;   /* next 33 bits */
+    const double PIO2_3 = 2.02226624871116645580e-21;   /* next 33 bits */
+    const double PIO2_3T = 8.47842766036889956997e-32;  /* tail */
+    double k = pt_libm_floor(x * INV_PIO2 + 0.5);
+    double r = x - k * PIO2_1;
+    r = r - k * PIO2_2;
+    r = r - k * PIO2_3;
+    r = r - k * PIO2_3T;
+    long long ki = (long long)k;
+    int q = (int)(ki & 3);
+    double s = pt_kernel_sin(r);
+    double c = pt_kernel_cos(r);
+    double so, co;
+    switch (q) {
+        case 0: so = s; co = c; break;
+        case 1: so = c; co = -s; break;
+        case 2: so = -s; co = -c; break;
+        default: so = -c; co = s; break;
+    }
+    *s_out = (float)so;
+    *c_out = (float)co;
+}
+
+PT_LIBM_FN float pt_sinf(float x) { float s, c; pt_sincosf(x, &s, &c); return s; }
+PT_LIBM_FN float pt_cosf(float x) { float s, c; pt_sincosf(x, &s, &c); return c; }
+
+/* powf(x, 5.0f) as used by FresnelSchlick (interactions.cu:197-201): x^5 in double, one rounding. */
+PT_LIBM_FN float pt_pow5f(float xf) {
+    double x = (double)xf;
+    double x2 = x * x;
+    double x4 = x2 * x2;
+    return (float)(x4 * x);
+}
+
+#endif /* PT_LIBM_H */

@@ -1,0 +1,24 @@
+#!/usr/bin/env bash
+# Builds the reference-pin harnesses into oracle/_ref/ (git-ignored) and regenerates the
+# committed fixtures under tests/golden/.  Needs /root/reference (this container only).
+#   rng_pin     : hipcc host build against rocThrust (the reference's RNG dependency)
+#   ingest_pin  : g++ build of the reference's own src/utilities.cpp + vendored glm / json
+set -euo pipefail
+HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
+REPO="$(cd "$HERE/../.." && pwd)"
+REF="${REF:-/root/reference}"
+OUT="$REPO/oracle/_ref"
+GOLD="$REPO/tests/golden"
+mkdir -p "$OUT" "$GOLD"
+hipcc -O1 -x hip --offload-arch=gfx950 "$HERE/rng_pin.cpp" -o "$OUT/rng_pin"
+g++ -std=c++17 -O2 -I "$REF/src" -I "$REF/external/include" "$HERE/ingest_pin.cpp" "$REF/src/utilities.cpp" \
+    -o "$OUT/ingest_pin"
+"$OUT/rng_pin" > "$GOLD/rng_pin.json"
+SCENES=$(ls "$REF"/scenes/*.json)
+"$OUT/ingest_pin" $SCENES | python3 -c '
+import json, os, sys
+d = json.load(sys.stdin)
+d["scenes"] = {os.path.basename(k): v for k, v in d["scenes"].items()}
+json.dump(d, sys.stdout, separators=(",", ":"))
+' > "$GOLD/ingest_pin.json"
+echo "fixtures written: $GOLD/rng_pin.json $GOLD/ingest_pin.json"
