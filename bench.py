@@ -1,0 +1,225 @@
+"""bench.py — BASELINE.json's headline: Mpaths/s (path segments traced per second) and ms/frame
+for scenes/cornell.json at 800x800, depth 8, stream compaction on (BASELINE configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pipeline fused|staged] [--no-cpu-baseline]
+
+A "step" is one pathtrace() frame: one sample for every pixel, all bounces, accumulated into the
+HBM-resident image (no host copy: pathtrace.cu's per-frame 7.68 MB D->H copy is outside `value`,
+its cost is reported separately as `pcie_ms_per_frame`).  With N > 1 (launched by
+torch.distributed.run, one rank per GPU) every rank traces full frames with its own iteration
+numbers (sample sharding, weak scaling: rank r traces iterations r+1, r+1+N, ...), and the
+accumulated framebuffers are summed to rank 0 with one RCCL reduce inside the timed region.
+
+Timing: W untimed frames, then barrier + device sync, K frames, device sync + barrier; the MAX over
+ranks of the elapsed time; value = segments traced by all ranks / that time.  The timed frames are
+launched eagerly with a HIP event after every kernel on the library's stream, which gives the
+dominant kernel's average duration for the `roofline` object (algorithmic bytes / duration).
+Everything traced is the real workload: the cornell scene from the reference's JSON, no work
+skipped.  rank 0 then times the CPU oracle (oracle/, a port of the reference path with
+stream_compaction/cpu.cu's compactWithScan) on a bounded sample for `cpu_baseline`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "project3-cuda-path-tracer-2025_amd")
+SCENE = os.path.join(REPO, "scenes", "cornell.json")
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
+REF_MS_PER_FRAME = 42.204      # reference README.md:136, RTX 3060 Laptop, compaction on
+STATE_BYTES = 48               # one path in flight: 3 x float4 (origin|pixel, dir|bounces, rgb|-)
+IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--pipeline", choices=["fused", "staged"], default="fused")
+    ap.add_argument("--scene", default=SCENE)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch                     # first: ptamd then shares torch's HIP runtime
+    import torch.distributed as dist
+    sys.path.insert(0, PKG)
+    import ptamd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    scene = ptamd.SceneFile(args.scene)
+    pipeline = ptamd.PIPELINE_STAGED if args.pipeline == "staged" else ptamd.PIPELINE_FUSED
+    tr = ptamd.PathTracer(scene, device=local, pipeline=pipeline)
+    depth = scene.trace_depth
+
+    # warmup: iterations 1..W on rank 0's schedule (r + 1 + k*world)
+    it = rank + 1
+    for _ in range(args.warmup):
+        tr.trace_frames(it, 1)
+        it += world
+    tr.synchronize()
+    tr.reset_stats()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()      # same HIP runtime as the library: covers its stream too
+        tr.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    if world == 1:
+        prof = tr.profile(it, args.steps)              # K frames, events after every kernel
+    else:
+        # each rank: its own iterations, interleaved sample schedule
+        prof = None
+        for k in range(args.steps):
+            tr.trace_frames(it + k * world, 1)
+        tr.synchronize()
+        ptr, n = tr.image_device_ptr()
+        img = _device_tensor(torch, ptr, n, local, tr)
+        dist.reduce(img, dst=0, op=dist.ReduceOp.SUM)   # one RCCL framebuffer combine
+        torch.cuda.synchronize()
+    tr.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = tr.stats()
+    segs = st["segments_total"]
+    frames = st["frames_total"]
+    assert frames == args.steps, (frames, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, segs = float(tmax[0]), float(t[1])
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = segs / elapsed / 1e6
+
+    if rank == 0:
+        line = {
+            "metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8",
+            "value": round(value, 2),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(REF_MS_PER_FRAME / ms_per_step, 2),
+            "vs_baseline_basis": "reference ms/frame 42.204 (README.md:136, RTX 3060 Laptop) / our ms_per_step",
+            "dtype": "f32",
+            "data": "scenes/cornell.json from the reference (800x800, depth 8, 1 spp per step); no synthetic inputs",
+            "config": {"workload": "cornell.json 800x800 depth 8, stream compaction on, sort off (BASELINE configs[1])",
+                       "pipeline": args.pipeline, "segments_per_frame": round(segs / args.steps / world, 1),
+                       "parallelism": f"sample-sharded x{world}" if world > 1 else "single GPU"},
+        }
+        if prof is not None:
+            line["roofline"] = roofline(prof, st, args, depth)
+            line["kernels_ms_per_frame"] = {"frame": round(prof["frame_ms"], 4),
+                                            "bounce": [round(x, 4) for x in prof["bounce_ms"]]}
+        line["pcie_ms_per_frame"] = pcie_copy_ms(tr)
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    tr.free()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _device_tensor(torch, ptr, n, device, tr):
+    """Zero-copy torch view of the library's image buffer (same HIP runtime)."""
+    class _Cai:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 2}
+    try:
+        return torch.as_tensor(_Cai(), device=f"cuda:{device}")
+    except Exception:
+        t = torch.from_numpy(tr.image().reshape(-1)).to(f"cuda:{device}")
+        return t
+
+
+def roofline(prof, st, args, depth):
+    """Dominant kernel = the fused bounce kernel (all `depth` launches of a frame, the same code):
+    algorithmic bytes per launch = 48 B per path read (bounce > 0) + 48 B per survivor written
+    + 24 B image read-modify-write per terminated path; / its average launch duration."""
+    tot = st["live_total"]                 # per-bounce live counts summed over the timed frames
+    k = st["frames_total"]
+    if args.pipeline == "fused":
+        nbytes = 0
+        for b in range(depth):
+            n_in, n_out = tot[b], tot[b + 1] if b + 1 < len(tot) else 0
+            nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + IMAGE_RMW_BYTES * (n_in - n_out)
+        launches = depth
+        ms = sum(prof["bounce_ms"][:depth])
+        name = "k_bounce (fused camera|intersect|shade|gather|compact, 8 launches per frame)"
+    else:
+        nbytes = sum(4 * tot[b] + 2 * STATE_BYTES * (tot[b + 1] if b + 1 < len(tot) else 0) for b in range(depth))
+        launches = depth
+        ms = prof["compact_ms"]
+        name = "k_compact (stable partition, decoupled look-back)"
+    bytes_per_launch = nbytes / (k * launches)
+    avg_ms = ms / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = _traffic(name)
+    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_ms, 5)}
+
+
+def _traffic(name):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*traffic*.json)."""
+    p = os.path.join(REPO, "profiles", "r01_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    key = "k_bounce" if name.startswith("k_bounce") else "k_compact"
+    return d.get(key, {}).get("hbm_bytes_per_launch")
+
+
+def pcie_copy_ms(tr):
+    """The reference copies the accumulated image to the host every frame (pathtrace.cu:783):
+    time one such copy."""
+    tr.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        tr.image()
+    return round((time.perf_counter() - t0) / 5 * 1e3, 3)
+
+
+def cpu_baseline(budget_s):
+    """The oracle (C port of the reference path: serial intersect/shade loops + cpu.cu's
+    compactWithScan) on this host, 1 thread, BASELINE configs[0] (cornell 400x400 depth 4)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    sc = O.load_scene(SCENE, res=(400, 400), depth=4)
+    r = O.Renderer(sc, O.options(num_threads=1))
+    segs, frames, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or frames < 2:
+        frames += 1
+        segs += int(np.maximum(r.trace(frames), 0).sum())
+    el = time.perf_counter() - t0
+    return {"value": round(segs / el / 1e6, 3), "unit": "Mpaths/s", "cores": 1, "kind": "port",
+            "sample": f"cornell.json 400x400 depth 4 (BASELINE configs[0]), {frames} frames in {el:.1f} s, "
+                      f"{el / frames * 1e3:.1f} ms/frame, oracle/pt_oracle.c single thread",
+            "ms_per_frame": round(el / frames * 1e3, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+/*
+ * pathtrace_abi.h — the drop-in C-ABI of the MI355X wavefront path tracer (libptamd.so).
+ *
+ * It replaces the reference's hot-path boundary, src/pathtrace.h:6-9:
+ *
+ *     void InitDataContainer(GuiDataContainer* guiData);   -> pt_init_data_container
+ *     void pathtraceInit(Scene* scene);                    -> pt_init   (+ C++ mirror in include/pathtrace.h)
+ *     void pathtraceFree();                                -> pt_free
+ *     void pathtrace(uchar4* pbo, int frame, int iteration)-> pt_trace
+ *
+ * with plain pointers + counts instead of the reference's Scene* (src/scene.h:6-28), and
+ * error codes instead of exit(EXIT_FAILURE) (pathtrace.cu:27-49).  The C++ mirror in
+ * include/pathtrace.h keeps the reference's exact void signatures on top of this ABI.
+ *
+ * State is process-global like the reference's file-static device buffers
+ * (pathtrace.cu:82-101); the library is not re-entrant.  All arrays are in the reference's
+ * own layouts (include/pt/scene_structs.h); the library converts them once, at pt_init, to
+ * its device layout.  Every function returns PT_OK (0) or a negative PT_E* code;
+ * pt_last_error() gives the message.
+ */
+#ifndef PT_PATHTRACE_ABI_H
+#define PT_PATHTRACE_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pt/scene_structs.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+enum {
+    PT_OK = 0,
+    PT_E_INVALID = -1,      /* bad argument / scene */
+    PT_E_STATE = -2,        /* call order (e.g. pt_trace before pt_init) */
+    PT_E_HIP = -3,          /* HIP runtime error */
+    PT_E_NODEVICE = -4,     /* no gfx950 device visible */
+    PT_E_UNSUPPORTED = -5
+};
+
+/* Flat view of the reference's Scene (src/scene.h:20-27).  Borrowed for the duration of
+ * pt_init only (the library copies what it needs to the device; the reference kept a
+ * non-owning Scene* and re-read traceDepth/camera each frame — pt_set_camera covers that). */
+typedef struct pt_scene_view {
+    const pt_geom* geoms;          int32_t num_geoms;
+    const pt_material* materials;  int32_t num_materials;
+    const pt_texture* textures;    int32_t num_textures;
+    const pt_triangle* triangles;  int32_t num_triangles;
+    const int32_t* tri_indices;    int32_t num_tri_indices;
+    const pt_bvh_node* bvh_nodes;  int32_t num_bvh_nodes;
+    pt_camera camera;
+    int32_t trace_depth;           /* RenderState::traceDepth */
+} pt_scene_view;
+
+enum { PT_PIPELINE_FUSED = 0, PT_PIPELINE_STAGED = 1 };
+enum { PT_SHARD_NONE = 0, PT_SHARD_PIXELS = 1, PT_SHARD_SAMPLES = 2 };
+
+typedef struct pt_options {
+    int32_t stream_compaction;   /* STREAM_COMPACTION (pathtrace.cu:21), default 1 */
+    int32_t material_sort;       /* MATERIAL_SORTING  (pathtrace.cu:22), default 0 */
+    int32_t bvh;                 /* BVH_ACCELERATION  (pathtrace.cu:24), default 1 */
+    int32_t arg_order;           /* 0: glm::vec2(u01(rng), u01(rng)) right-to-left (g++), 1: left-to-right */
+    int32_t pipeline;            /* PT_PIPELINE_FUSED (default) or PT_PIPELINE_STAGED (one kernel per stage) */
+    int32_t use_graph;           /* capture a frame in a hipGraph and replay it (default 1) */
+    int32_t device;              /* HIP device ordinal (default 0) */
+    int32_t shard_mode;          /* PT_SHARD_*: multi-GPU partition of one frame (default NONE) */
+    int32_t shard_rank;
+    int32_t shard_count;
+    int32_t shard_rows;          /* PIXELS mode: height of the interleaved row bands (default 8) */
+    int32_t block_size;          /* threads per block of the per-path kernels (default 256) */
+} pt_options;
+
+typedef struct pt_frame_stats {
+    int32_t iteration;           /* iteration of the last traced frame */
+    int32_t bounces;             /* trace depth */
+    int64_t live[64];            /* paths entering bounce b (b < bounces) */
+    int64_t segments;            /* sum of live[] = the metric's path segments */
+    int64_t pixels;              /* pixels traced by this process */
+    int64_t frames_total;        /* frames traced since pt_init / pt_reset_stats */
+    int64_t live_total[65];      /* per-bounce live counts summed over those frames */
+    int64_t segments_total;      /* path segments traced over those frames */
+} pt_frame_stats;
+
+int32_t pt_abi_version(void);
+const char* pt_last_error(void);
+void pt_default_options(pt_options* opts);
+
+/* InitDataContainer (pathtrace.cu:103-106): `traced_depth` (GuiDataContainer::TracedDepth)
+ * receives the number of bounces traced after each pt_trace; NULL disables. */
+int32_t pt_init_data_container(int32_t* traced_depth);
+
+/* pathtraceInit (pathtrace.cu:134-207): upload the scene, size the wavefront for
+ * camera.resolution, zero the accumulated image.  Calling it again re-initialises. */
+int32_t pt_init(const pt_scene_view* scene, const pt_options* opts);
+
+/* pathtraceFree (pathtrace.cu:209-229). Safe to call when not initialised. */
+int32_t pt_free(void);
+
+/* pathtrace(pbo, frame, iteration) (pathtrace.cu:639-787): trace one sample per pixel with
+ * 1-based `iteration`, add it into the accumulated image, write the 8-bit preview into
+ * `pbo_device` (a DEVICE pointer of width*height pt_uchar4, or NULL), and copy the
+ * accumulated (not averaged) image into `host_image` (width*height*3 floats, or NULL) —
+ * the reference copies into scene->state.image every call (pathtrace.cu:783-784). */
+int32_t pt_trace(pt_uchar4* pbo_device, int32_t frame, int32_t iteration, float* host_image);
+
+/* Trace `count` frames with iterations first_iteration .. first_iteration+count-1, image stays
+ * in HBM (no host copy, no PBO).  The throughput path used by bench.py. */
+int32_t pt_trace_frames(int32_t first_iteration, int32_t count);
+
+/* Block until all queued work finished. */
+int32_t pt_synchronize(void);
+
+/* Accumulated image: host copy (n_floats >= width*height*3) / raw device pointer. */
+int32_t pt_get_image(float* host_out, int64_t n_floats);
+int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats);
+/* Overwrite the accumulated image (host data), e.g. after a multi-GPU reduce. */
+int32_t pt_set_image(const float* host_in, int64_t n_floats);
+
+int32_t pt_get_frame_stats(pt_frame_stats* out);
+/* Zero the running totals of pt_frame_stats (frames_total, live_total, segments_total). */
+int32_t pt_reset_stats(void);
+
+/* Camera update without re-upload (main.cpp:423-444 path); resets nothing else. */
+int32_t pt_set_camera(const pt_camera* camera);
+
+/* ---- scene ingest (C++ restatement of scene.cpp, host/scene.cpp) for non-C++ callers ---- */
+typedef struct pt_scene_file pt_scene_file;
+/* Load a reference JSON scene.  res_x/res_y <= 0 / depth < 0 keep the file's RES/DEPTH (overriding
+ * them recomputes pixelLength exactly as editing the file would).  viewer_camera != 0 applies
+ * main.cpp:359-380 + 423-444, the camera the reference's frames are rendered with. */
+int32_t pt_scene_load(const char* json_path, int32_t res_x, int32_t res_y, int32_t depth, int32_t viewer_camera,
+                      pt_scene_file** out);
+/* View borrowed from the scene file (valid until pt_scene_free). */
+int32_t pt_scene_get_view(const pt_scene_file* scene, pt_scene_view* view);
+int32_t pt_scene_get_info(const pt_scene_file* scene, int32_t* iterations, int32_t* trace_depth, char* image_name,
+                          int32_t cap);
+int32_t pt_scene_material_name(const pt_scene_file* scene, int32_t id, char* buf, int32_t cap);
+void pt_scene_free(pt_scene_file* scene);
+const char* pt_scene_last_error(void);
+
+/* ---- test entry points: run one production kernel on caller data (reference layouts) ---- */
+/* generateRayFromCamera for every pixel of this process's shard -> out[pixels] */
+int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n);
+/* computeIntersections on n paths -> isects (zeroed + t=-1 semantics of pathtrace.cu:699,423) */
+int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_isect* isects);
+/* kernShadeMaterialProper on n (isect, path) pairs, in place; terminated paths are NOT
+ * gathered (image untouched) */
+int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_path_segment* paths, int64_t n);
+/* stable partition of n paths on remainingBounces > 0 -> out (alive first, in order);
+ * returns the alive count through *alive */
+int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment* out, int64_t* alive);
+/* stable sort of n (isect, path) pairs by materialId -> permutation perm[n] */
+int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm);
+/* first n draws of makeSeededRandomEngine(iter, index, depth) for m seeds -> out[m*n] */
+int32_t pt_test_rng(const int32_t* iter_index_depth, int64_t m, int32_t n, float* out);
+/* sendImageToPBO on a caller image (host, n pixels) -> pbo (host) */
+int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4* pbo);
+
+/* ---- kernel timing (HIP events on the library's stream) for bench.py ---- */
+typedef struct pt_kernel_times {
+    int32_t frames;
+    float frame_ms;              /* average frame wall time between events */
+    float bounce_ms[64];         /* average per-bounce kernel time (fused) / per-stage sums (staged) */
+    float compact_ms;            /* staged: total compaction-kernel time per frame */
+    float intersect_ms, shade_ms, camera_ms, sort_ms;
+    int64_t compact_bytes;       /* algorithmic bytes moved by compaction per frame */
+    int64_t frame_bytes;         /* algorithmic bytes of the whole frame */
+} pt_kernel_times;
+/* Trace `count` frames with iterations first_iteration.. eagerly, a HIP event recorded on the
+ * library's stream after every kernel and no host synchronisation until all frames are queued;
+ * returns per-kernel average durations.  bounce_ms[b]: fused bounce kernel b, or (staged) the
+ * compaction kernel of bounce b. */
+int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_times* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_PATHTRACE_ABI_H */

@@ -309,7 +309,7 @@ def load_scene(path: str, res=None, depth=None, obj_dir: str | None = None) -> S
     tdepth = cam["DEPTH"] if depth is None else depth
     camera = np.zeros(1, CAMERA)
     L.or_camera_setup(int(rx), int(ry), float(cam["FOVY"]), v3(cam["EYE"]), v3(cam["LOOKAT"]), v3(cam["UP"]),
-                      float(cam["APERTURE"]), camera.ctypes.data)
+                      float(cam.get("APERTURE", 0.0)), camera.ctypes.data)
     triangles = np.concatenate(tris) if tris else np.zeros(0, TRIANGLE)
     if len(triangles):
         nodes = np.zeros(max(1, 2 * len(triangles)), BVHNODE)

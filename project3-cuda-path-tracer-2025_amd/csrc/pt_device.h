@@ -1,0 +1,513 @@
+// pt_device.h — device-side building blocks of the wavefront path tracer (gfx950).
+//
+// Everything here is a __device__ restatement of the reference's per-path math with the
+// exact IEEE operation order of the reference (glm 0.9.6 semantics, see DESIGN.md "Numerics"),
+// so that — compiled with -ffp-contract=off, IEEE division/sqrt and the shared pt_libm trig —
+// each path is bit-identical to the CPU oracle's.  Reference citations are file:line in
+// /root/reference/src.
+//
+// Data layout choices (MI355X-first, not the reference's AoS):
+//   * scene constants (geoms, BVH nodes, hot triangles) are read through wave-uniform or
+//     cache-resident loads; geoms are pre-reduced to the 3 affine rows of each matrix;
+//   * a path in flight is 3 x float4 (origin|pixel, direction|bounces, throughput|-),
+//     each float4 stream contiguous across paths so one wave moves 1 KiB per instruction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt/pt_libm.h"
+#include "pt/scene_structs.h"
+
+#define PT_DEV __device__ __forceinline__
+
+namespace ptd {
+
+// utilities.h:13-20
+constexpr float PI = 3.1415926535897932384626422832795028841971f;
+constexpr float TWO_PI = 6.2831853071795864769252867665590057683943f;
+constexpr float PI_OVER_FOUR = 0.78539816339744831f;
+constexpr float PI_OVER_TWO = 1.57079632679489662f;
+constexpr float INV_PI = 0.31830988618379067154f;
+constexpr float BABY_EPSILON = 0.00001f;
+constexpr float LARGER_EPSILON = 0.001f;
+constexpr float FLT_MAX_ = 3.402823466e+38f;
+
+// ------------------------------------------------------------------------------------------
+// float3 with glm 0.9.6 semantics
+// ------------------------------------------------------------------------------------------
+struct f3 {
+    float x, y, z;
+};
+PT_DEV f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+PT_DEV f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+PT_DEV f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+PT_DEV f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+PT_DEV f3 operator*(f3 a, float s) { return f3{a.x * s, a.y * s, a.z * s}; }
+PT_DEV f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+PT_DEV f3 operator/(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+PT_DEV f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+// compute_dot<tvec3>: (x*y).x + .y + .z, left to right
+PT_DEV float dot(f3 a, f3 b) {
+    float px = a.x * b.x, py = a.y * b.y, pz = a.z * b.z;
+    return px + py + pz;
+}
+PT_DEV f3 cross(f3 x, f3 y) {
+    return f3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y};
+}
+PT_DEV float length(f3 v) { return __builtin_sqrtf(dot(v, v)); }
+// normalize = x * (1 / sqrt(dot(x, x)))  (func_geometric.inl:158, func_exponential.inl:150-153)
+PT_DEV f3 normalize(f3 v) { return v * (1.0f / __builtin_sqrtf(dot(v, v))); }
+PT_DEV f3 reflect(f3 I, f3 N) { return I - (N * dot(N, I)) * 2.0f; }
+// glm 0.9.6 refract: NaN (not 0) on total internal reflection
+PT_DEV f3 refract(f3 I, f3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    f3 a = eta * I;
+    f3 b = (eta * d + __builtin_sqrtf(k)) * N;
+    return (a - b) * (float)(k >= 0.0f);
+}
+PT_DEV float gmin(float x, float y) { return x < y ? x : y; }
+PT_DEV float gmax(float x, float y) { return x > y ? x : y; }
+PT_DEV float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+PT_DEV f3 mix(f3 x, f3 y, float a) { return x + a * (y - x); }
+PT_DEV float comp(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+// ------------------------------------------------------------------------------------------
+// device scene records
+// ------------------------------------------------------------------------------------------
+// Affine part of a glm mat4: rows 0..2 of the 4 columns, column-major (m[c*3 + r]).
+struct Aff {
+    float m[12];
+};
+// glm mat4 * vec4, keeping the w term even when w == 0 (exact signed-zero behaviour):
+// r[i] = (m0[i]*x + m1[i]*y) + (m2[i]*z + m3[i]*w)
+PT_DEV f3 xform(const float* m, f3 v, float w) {
+    float r0 = (m[0] * v.x + m[3] * v.y) + (m[6] * v.z + m[9] * w);
+    float r1 = (m[1] * v.x + m[4] * v.y) + (m[7] * v.z + m[10] * w);
+    float r2 = (m[2] * v.x + m[5] * v.y) + (m[8] * v.z + m[11] * w);
+    return f3{r0, r1, r2};
+}
+
+// 160-byte geom: inverseTransform | transform | invTranspose (affine rows) + type + material
+struct DevGeom {
+    float inv[12];
+    float fwd[12];
+    float itr[12];
+    int32_t type;
+    int32_t materialid;
+    int32_t _pad[2];
+};
+static_assert(sizeof(DevGeom) == 160, "DevGeom");
+
+// 48-byte material: only what shading reads (sceneStructs.h:36-57)
+struct DevMaterial {
+    float color[3];
+    float emittance;
+    float hasReflective, hasRefractive, roughness, metallic;
+    float ior;
+    int32_t hasTexture;
+    int32_t textureID;
+    int32_t _pad;
+};
+static_assert(sizeof(DevMaterial) == 48, "DevMaterial");
+
+// 32-byte BVH node: (min.xyz, a) (max.xyz, b); internal: a = left, b = right (<0: none);
+// leaf (reference: triCount > 0 && start >= 0): a = start, b = -(triCount + 2)
+struct DevNode {
+    float4 lo;
+    float4 hi;
+};
+
+// hot triangle record in leaf order (index k = node.start + i): 3 positions, 48 bytes
+struct DevTriHot {
+    float4 a;   // v0.xyz, v1.x
+    float4 b;   // v1.yz, v2.xy
+    float4 c;   // v2.z, triIndex (int bits), -, -
+};
+
+// cold triangle data, by reference triangle index (read once for the winner)
+struct DevTriCold {
+    float n0[3], n1[3], n2[3];   // vertex normals
+    float uv0[2], uv1[2], uv2[2];
+    float dpdu[3], dpdv[3];
+    int32_t materialID;
+    int32_t _pad;
+};
+
+// ------------------------------------------------------------------------------------------
+// RNG: utilhash (intersections.h:13-22) + thrust::minstd_rand + uniform_real_distribution<float>
+// ------------------------------------------------------------------------------------------
+PT_DEV uint32_t utilhash(uint32_t a) {
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return a;
+}
+struct Rng {
+    uint32_t x;
+};
+// makeSeededRandomEngine(iter, index, depth), pathtrace.cu:51-56
+PT_DEV Rng rng_make(int iter, int index, int depth) {
+    uint32_t h = utilhash(0x80000000u | ((uint32_t)depth << 22) | (uint32_t)iter) ^ utilhash((uint32_t)index);
+    uint32_t x = h % 2147483647u;
+    return Rng{x == 0u ? 1u : x};
+}
+// x <- 48271 * x mod (2^31 - 1), exact via the Mersenne fold
+PT_DEV uint32_t rng_next(Rng& r) {
+    uint64_t p = (uint64_t)r.x * 48271ull;
+    uint32_t s = (uint32_t)(p & 0x7fffffffull) + (uint32_t)(p >> 31);
+    if (s >= 2147483647u) s -= 2147483647u;
+    r.x = s;
+    return s;
+}
+// float(x - 1) / (1 + float(max - min)) == float(x - 1) * 2^-31 exactly
+PT_DEV float u01(Rng& r) { return (float)(rng_next(r) - 1u) * 4.656612873077392578125e-10f; }
+
+// ------------------------------------------------------------------------------------------
+// primitives (intersections.cu)
+// ------------------------------------------------------------------------------------------
+// getPointOnRay, intersections.h:29-32
+PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize(d); }
+
+// boxIntersectionTest, intersections.cu:3-57.  Returns t; `seed` receives the object-space
+// normal (tmin_n) the winner's world normal is derived from.
+PT_DEV float box_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
+    f3 qo = xform(g.inv, ro, 1.0f);
+    f3 qd = normalize(xform(g.inv, rd, 0.0f));
+    float tmin = -1e38f, tmax = 1e38f;
+    f3 tmin_n = mk(0.f, 0.f, 0.f), tmax_n = mk(0.f, 0.f, 0.f);
+#pragma unroll
+    for (int xyz = 0; xyz < 3; ++xyz) {
+        float qdx = comp(qd, xyz), qox = comp(qo, xyz);
+        float t1 = (-0.5f - qox) / qdx;
+        float t2 = (+0.5f - qox) / qdx;
+        float ta = gmin(t1, t2);
+        float tb = gmax(t1, t2);
+        float s = t2 < t1 ? +1.0f : -1.0f;
+        f3 n = mk(xyz == 0 ? s : 0.f, xyz == 1 ? s : 0.f, xyz == 2 ? s : 0.f);
+        if (ta > 0 && ta > tmin) { tmin = ta; tmin_n = n; }
+        if (tb < tmax) { tmax = tb; tmax_n = n; }
+    }
+    if (tmax >= tmin && tmax > 0) {
+        if (tmin <= 0) { tmin = tmax; tmin_n = tmax_n; }
+        f3 p = xform(g.fwd, point_on_ray(qo, qd, tmin), 1.0f);
+        seed = tmin_n;
+        return length(ro - p);
+    }
+    return -1.0f;
+}
+
+// sphereIntersectionTest, intersections.cu:59-109.  `seed` = object-space hit point.
+PT_DEV float sphere_test(const DevGeom& g, f3 ro_w, f3 rd_w, f3& seed) {
+    f3 ro = xform(g.inv, ro_w, 1.0f);
+    f3 rd = normalize(xform(g.inv, rd_w, 0.0f));
+    float vDotDirection = dot(ro, rd);
+    float radicand = vDotDirection * vDotDirection - (dot(ro, ro) - 0.25f);  // powf(.5, 2) == .25
+    if (radicand < 0) return -1.0f;
+    float squareRoot = __builtin_sqrtf(radicand);
+    float firstTerm = -vDotDirection;
+    float t1 = firstTerm + squareRoot;
+    float t2 = firstTerm - squareRoot;
+    float t;
+    if (t1 < 0 && t2 < 0) return -1.0f;
+    else if (t1 > 0 && t2 > 0) t = gmin(t1, t2);
+    else t = gmax(t1, t2);
+    f3 objp = point_on_ray(ro, rd, t);
+    f3 p = xform(g.fwd, objp, 1.0f);
+    seed = objp;
+    return length(ro_w - p);
+}
+
+// Moller-Trumbore, intersections.cu:112-145
+PT_DEV bool tri_test(f3 ro, f3 rd, f3 v0, f3 v1, f3 v2, float& tOut, float& uOut, float& vOut) {
+    f3 edge1 = v1 - v0;
+    f3 edge2 = v2 - v0;
+    f3 pvec = cross(rd, edge2);
+    float det = dot(edge1, pvec);
+    if (__builtin_fabsf(det) < BABY_EPSILON) return false;
+    float invDet = 1.0f / det;
+    f3 tvec = ro - v0;
+    float u = dot(tvec, pvec) * invDet;
+    if (u < 0.0f || u > 1.0f) return false;
+    f3 qvec = cross(tvec, edge1);
+    float v = dot(rd, qvec) * invDet;
+    if (v < 0.0f || (u + v) > 1.0f) return false;
+    float t = dot(edge2, qvec) * invDet;
+    if (t <= BABY_EPSILON) return false;
+    tOut = t; uOut = u; vOut = v;
+    return true;
+}
+
+// aabbIntersectionTest, intersections.cu:237-275
+PT_DEV bool aabb_test(float4 lo, float4 hi, f3 ro, f3 rd) {
+    float t_min = -FLT_MAX_, t_max = FLT_MAX_;
+    const float bmin[3] = {lo.x, lo.y, lo.z};
+    const float bmax[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        float dir = comp(rd, i), origin = comp(ro, i);
+        if (__builtin_fabsf(dir) < 0.00001f) {
+            if (origin < bmin[i] || origin > bmax[i]) return false;
+        } else {
+            float t1 = (bmin[i] - origin) / dir;
+            float t2 = (bmax[i] - origin) / dir;
+            if (t1 > t2) { float tmp = t1; t1 = t2; t2 = tmp; }
+            if (t1 > t_min) t_min = t1;
+            if (t2 < t_max) t_max = t2;
+            if (t_min > t_max) return false;
+        }
+    }
+    return t_max >= t_min && t_max > 0.f;
+}
+
+// ------------------------------------------------------------------------------------------
+// BSDFs (interactions.h / interactions.cu)
+// ------------------------------------------------------------------------------------------
+struct M3 {
+    f3 c0, c1, c2;   // columns
+};
+PT_DEV f3 mul(const M3& m, f3 v) {
+    return f3{m.c0.x * v.x + m.c1.x * v.y + m.c2.x * v.z, m.c0.y * v.x + m.c1.y * v.y + m.c2.y * v.z,
+              m.c0.z * v.x + m.c1.z * v.y + m.c2.z * v.z};
+}
+// transpose(M) * v
+PT_DEV f3 mulT(const M3& m, f3 v) {
+    return f3{m.c0.x * v.x + m.c0.y * v.y + m.c0.z * v.z, m.c1.x * v.x + m.c1.y * v.y + m.c1.z * v.z,
+              m.c2.x * v.x + m.c2.y * v.y + m.c2.z * v.z};
+}
+// coordinateSystem + LocalToWorld, interactions.h:14-27
+PT_DEV M3 local_to_world(f3 n) {
+    f3 t;
+    if (__builtin_fabsf(n.x) > __builtin_fabsf(n.y))
+        t = mk(-n.z, 0, n.x) / __builtin_sqrtf(n.x * n.x + n.z * n.z);
+    else
+        t = mk(0, n.z, -n.y) / __builtin_sqrtf(n.y * n.y + n.z * n.z);
+    return M3{t, cross(n, t), n};
+}
+
+// glm::vec2(u01(rng), u01(rng)): argument evaluation order is the compiler's (arg_order 0 =
+// right-to-left as g++ does, 1 = left-to-right)
+PT_DEV void u01_pair(Rng& r, int arg_order, float& x, float& y) {
+    float a = u01(r);
+    float b = u01(r);
+    x = arg_order ? a : b;
+    y = arg_order ? b : a;
+}
+
+// squareToDiskConcentric + squareToHemisphereCosine, interactions.cu:49-85
+PT_DEV f3 hemisphere_cosine(float xi0, float xi1) {
+    float x, y;
+    if (xi0 == 0.f && xi1 == 0.f) {
+        x = 0.f; y = 0.f;
+    } else {
+        float theta, radius;
+        float a = (2.f * xi0) - 1.f;
+        float b = (2.f * xi1) - 1.f;
+        if ((a * a) > (b * b)) {
+            radius = 1.f * a;
+            theta = PI_OVER_FOUR * (b / a);
+        } else {
+            radius = 1.f * b;
+            theta = PI_OVER_TWO - (PI_OVER_FOUR * (a / b));
+        }
+        float s, c;
+        pt_sincosf(theta, &s, &c);
+        x = radius * c;
+        y = radius * s;
+    }
+    float z = __builtin_sqrtf(gmax(0.f, 1.0f - (x * x) - (y * y)));
+    return mk(x, y, z);
+}
+
+// sampleFDiffuse, interactions.cu:92-108 (returns bsdf; pdf, wiW out)
+PT_DEV f3 sample_diffuse(f3 albedo, f3 normal, f3& wiW, float& pdf, Rng& rng, int arg_order) {
+    float xi0, xi1;
+    u01_pair(rng, arg_order, xi0, xi1);
+    f3 wi = hemisphere_cosine(xi0, xi1);
+    M3 ws = local_to_world(normal);
+    wiW = normalize(mul(ws, wi));
+    pdf = wi.z / PI;
+    return albedo * INV_PI;
+}
+
+// sampleFSpecularTrans, interactions.cu:146-168
+PT_DEV f3 sample_spec_trans(f3 albedo, f3 normal, f3 wo, float IOR, f3& wiW) {
+    bool entering = dot(wo, normal) < 0.0f;
+    float eta = entering ? (1.0f / IOR) : IOR;
+    f3 outNormal = entering ? normal : -normal;
+    wiW = refract(normalize(wo), normalize(outNormal), eta);
+    if (length(wiW) < BABY_EPSILON) {
+        wiW = reflect(wo, normal);
+        return mk(0.f, 0.f, 0.f);
+    }
+    return albedo;
+}
+
+// FresnelDielectricEval, interactions.cu:173-194
+PT_DEV float fresnel_dielectric(float cosThetaI, float IOR) {
+    float etaI = 1.f, etaT = IOR;
+    cosThetaI = gclamp(cosThetaI, -1.f, 1.f);
+    if (cosThetaI > 0.f) { float tmp = etaI; etaI = etaT; etaT = tmp; }
+    cosThetaI = __builtin_fabsf(cosThetaI);
+    float sinThetaI = __builtin_sqrtf(gmax(0.f, 1.f - cosThetaI * cosThetaI));
+    float sinThetaT = etaI / etaT * sinThetaI;
+    float cosThetaT = __builtin_sqrtf(gmax(0.f, 1.f - sinThetaT * sinThetaT));
+    float Rparl = ((etaT * cosThetaI) - (etaI * cosThetaT)) / ((etaT * cosThetaI) + (etaI * cosThetaT));
+    float Rperp = ((etaI * cosThetaI) - (etaT * cosThetaT)) / ((etaI * cosThetaI) + (etaT * cosThetaT));
+    return (Rparl * Rparl + Rperp * Rperp) * 0.5f;
+}
+
+// FresnelSchlick, interactions.cu:197-201
+PT_DEV f3 fresnel_schlick(float cosTheta, f3 F0) {
+    float p = pt_pow5f(1.0f - cosTheta);
+    return mk(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
+}
+
+// sampleFGlass, interactions.cu:204-235
+PT_DEV f3 sample_glass(f3 albedo, f3 normal, f3 wo, float IOR, f3& wiW, Rng& rng) {
+    float random = u01(rng);
+    float fresnel = fresnel_dielectric(dot(wo, normal), IOR);
+    if (random < fresnel) {
+        wiW = reflect(wo, normal);
+        return albedo;
+    }
+    f3 T = sample_spec_trans(albedo, normal, wo, IOR, wiW);
+    if (length(wiW) < BABY_EPSILON) {
+        wiW = reflect(wo, normal);
+        return albedo;
+    }
+    return T;
+}
+
+// microfacet trig helpers, interactions.h:106-167
+PT_DEV float cos2t(f3 w) { return w.z * w.z; }
+PT_DEV float sin2t(f3 w) { return gmax(0.f, 1.f - cos2t(w)); }
+PT_DEV float tan2t(f3 w) { return sin2t(w) / cos2t(w); }
+PT_DEV float sint(f3 w) { return __builtin_sqrtf(sin2t(w)); }
+PT_DEV float tant(f3 w) { return sint(w) / w.z; }
+PT_DEV float cosphi(f3 w) { float s = sint(w); return (s == 0) ? 0.f : gclamp(w.x / s, -1.f, 1.f); }
+PT_DEV float sinphi(f3 w) { float s = sint(w); return (s == 0) ? 0.f : gclamp(w.y / s, -1.f, 1.f); }
+
+// sampleWH, interactions.cu:238-264
+PT_DEV f3 sample_wh(f3 wo, float roughness, Rng& rng, int arg_order) {
+    float xi0, xi1;
+    u01_pair(rng, arg_order, xi0, xi1);
+    float phi = TWO_PI * xi1;
+    float tanTheta2 = roughness * roughness * xi0 / (1.0f - xi0);
+    float cosTheta = 1.0f / __builtin_sqrtf(1.0f + tanTheta2);
+    float sinTheta = __builtin_sqrtf(gmax(0.f, 1.f - cosTheta * cosTheta));
+    float s, c;
+    pt_sincosf(phi, &s, &c);
+    f3 wh = mk(sinTheta * c, sinTheta * s, cosTheta);
+    if (!(wo.z * wh.z > 0)) wh = -wh;
+    return wh;
+}
+// TrowbridgeReitzD, interactions.cu:266-283
+PT_DEV float tr_d(f3 wh, float r) {
+    float tan2Theta = tan2t(wh);
+    if (__builtin_isinf(tan2Theta)) return 0.f;
+    float cos4Theta = cos2t(wh) * cos2t(wh);
+    float cp = cosphi(wh), sp = sinphi(wh);
+    float e = ((cp * cp) / (r * r) + (sp * sp) / (r * r)) * tan2Theta;
+    return 1.0f / (PI * r * r * cos4Theta * (1.0f + e) * (1.0f + e));
+}
+// lambda, interactions.cu:285-297
+PT_DEV float tr_lambda(f3 w, float r) {
+    float absTanTheta = __builtin_fabsf(tant(w));
+    if (__builtin_isinf(absTanTheta)) return 0.f;
+    float a = (r * absTanTheta) * (r * absTanTheta);
+    return (-1.0f + __builtin_sqrtf(1.f + a)) / 2.0f;
+}
+// fMicrofacetRefl, interactions.cu:314-348
+PT_DEV f3 f_microfacet(f3 albedo, f3 wo, f3 wi, float r, float metallic) {
+    float cosThetaO = __builtin_fabsf(wo.z);
+    float cosThetaI = __builtin_fabsf(wi.z);
+    f3 wh = wi + wo;
+    if (cosThetaI == 0 || cosThetaO == 0) return mk(0.f, 0.f, 0.f);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return mk(0.f, 0.f, 0.f);
+    wh = normalize(wh);
+    f3 F0 = mix(mk(0.04f, 0.04f, 0.04f), albedo, metallic);
+    f3 F = fresnel_schlick(dot(wi, wh), F0);
+    float D = tr_d(wh, r);
+    float G = 1.0f / (1.0f + tr_lambda(wo, r) + tr_lambda(wi, r));
+    return (F * (D * G)) / (4.0f * cosThetaI * cosThetaO);
+}
+// sampleFMicrofacetRefl, interactions.cu:350-380
+PT_DEV f3 sample_microfacet(f3 albedo, f3 normal, f3 wo, float r, float metallic, f3& wiW, float& pdf,
+                            Rng& rng, int arg_order) {
+    M3 l2w = local_to_world(normal);
+    f3 wo_local = mulT(l2w, wo);
+    f3 wh_local = sample_wh(wo_local, r, rng, arg_order);
+    if (wh_local.z < 0.0f) wh_local = -wh_local;
+    f3 wi_local = reflect(-wo_local, wh_local);
+    wiW = normalize(mul(l2w, wi_local));
+    float dotWO_WH = gmax(dot(wo_local, wh_local), 1e-6f);
+    pdf = (tr_d(wh_local, r) * __builtin_fabsf(wh_local.z)) / (4.0f * dotWO_WH);
+    return f_microfacet(albedo, wo_local, wi_local, r, metallic);
+}
+// sampleFCookTorrance, interactions.cu:383-435
+PT_DEV f3 sample_cook_torrance(f3 albedo, f3 normal, f3 woW, float r, float metallic, f3& wiW, float& out_pdf,
+                               Rng& rng, int arg_order) {
+    f3 F0 = mix(mk(0.04f, 0.04f, 0.04f), albedo, metallic);
+    float cosTheta = gclamp(dot(normal, woW), 0.0f, 1.0f);
+    f3 F = fresnel_schlick(cosTheta, F0);
+    float Fprob = gclamp(gmax(F.x, gmax(F.y, F.z)), 0.0f, 1.0f);
+    float choose = u01(rng);
+    f3 bsdf;
+    float pdf_spec = 0.0f, pdf_diff = 0.0f;
+    bool spec = choose < Fprob;
+    if (spec) bsdf = sample_microfacet(albedo, normal, woW, r, metallic, wiW, pdf_spec, rng, arg_order);
+    else bsdf = sample_diffuse(albedo, normal, wiW, pdf_diff, rng, arg_order);
+    out_pdf = Fprob * pdf_spec + (1.0f - Fprob) * pdf_diff;
+    return spec ? bsdf * F : bsdf * (mk(1.0f, 1.0f, 1.0f) - F);
+}
+
+// ------------------------------------------------------------------------------------------
+// scatterRay (interactions.cu:438-542) on a path held in registers
+// ------------------------------------------------------------------------------------------
+struct PathReg {
+    f3 o, d, c;
+    int pix;
+    int rb;
+};
+
+PT_DEV void scatter(PathReg& p, f3 intersect, f3 normal, const DevMaterial& m, f3 mcolor, Rng& rng, int arg_order) {
+    f3 wiW = mk(0.f, 0.f, 0.f), bsdf;
+    float pdf = 1.0f;
+    if (m.hasRefractive > 0.0f && m.hasReflective > 0.0f) {          // Glass
+        bsdf = sample_glass(mcolor, normal, p.d, m.ior, wiW, rng);
+        p.d = normalize(wiW);
+        p.o = intersect + p.d * LARGER_EPSILON;
+        p.c = p.c * bsdf;
+    } else if (m.hasReflective > 0.0f) {                              // Mirror
+        wiW = reflect(p.d, normal);
+        p.d = normalize(wiW);
+        p.o = intersect + normal * BABY_EPSILON;
+        p.c = p.c * mcolor;
+    } else if (m.hasRefractive > 0.0f) {                              // Transmissive
+        bsdf = sample_spec_trans(mcolor, normal, p.d, m.ior, wiW);
+        p.d = normalize(wiW);
+        p.o = intersect + p.d * LARGER_EPSILON;
+        p.c = p.c * bsdf;
+    } else if (m.roughness >= 0.0f && m.metallic >= 0.0f) {           // Microfacet
+        f3 woW = -normalize(p.d);
+        bsdf = sample_cook_torrance(mcolor, normal, woW, m.roughness, m.metallic, wiW, pdf, rng, arg_order);
+        p.d = normalize(wiW);
+        p.o = intersect + p.d * LARGER_EPSILON;
+        float cosTheta = gmax(0.0f, dot(normal, wiW));
+        if (pdf > 0.0f) p.c = p.c * ((bsdf * cosTheta) / pdf);
+    } else {                                                          // Diffuse
+        bsdf = sample_diffuse(mcolor, normal, wiW, pdf, rng, arg_order);
+        p.d = normalize(wiW);
+        p.o = intersect + normal * BABY_EPSILON;
+        float cosTheta = gmax(0.0f, dot(normal, wiW));
+        p.c = p.c * ((bsdf * cosTheta) / pdf);
+    }
+    p.rb -= 1;
+}
+
+}  // namespace ptd

@@ -1,0 +1,258 @@
+// pt_kernels.h — per-path stage functions shared by the fused and the staged pipelines.
+//
+//   camera_ray      generateRayFromCamera         pathtrace.cu:231-292
+//   intersect_scene computeIntersections          pathtrace.cu:298-448 (+ intersections.cu)
+//   shade_path      kernShadeMaterialProper       pathtrace.cu:521-621 (+ interactions.cu)
+//
+// Each is a pure function of (scene, path, iteration), so the fused bounce kernel and the
+// one-kernel-per-stage pipeline run literally the same code.
+#pragma once
+
+#include "pt_device.h"
+
+namespace ptd {
+
+constexpr int NSEG = 8;        // output segments of the fused compaction (one per XCD group)
+constexpr int MAXB = 64;       // max trace depth supported by the frame control block
+constexpr int BLOCK = 256;     // threads per block of the per-path kernels
+constexpr int MAXSTACK = 64;   // reference BVH stack (intersections.cu:167)
+
+struct CamDev {
+    int resx, resy;
+    f3 position, view, up, right;
+    float plx, ply;
+    float aperture, focalDist;
+};
+
+struct ShardDev {
+    int mode;          // PT_SHARD_*
+    int rank, count, rows;
+    int local_pixels;
+};
+
+struct SceneDev {
+    const DevGeom* geoms;
+    const DevMaterial* mats;
+    const DevNode* nodes;
+    const DevTriHot* hot;
+    const DevTriCold* cold;
+    int num_geoms, num_mats, num_nodes, num_tris;
+    int trace_depth, arg_order, use_bvh, stack_depth;
+    CamDev cam;
+    ShardDev shard;
+};
+
+// frame control block (device memory); zeroed / advanced by k_frame_begin every frame
+struct FrameCtl {
+    int iter;
+    int _pad[3];
+    unsigned long long frames;              // frames started since the last stats reset
+    unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
+    int ticket[MAXB];                       // dynamic tile ids of the staged compaction kernel
+    int cnt[MAXB + 1][NSEG];                // paths entering bounce b, per output segment
+};
+
+// a wavefront of paths: three float4 streams
+struct PathBuf {
+    float4* A;   // origin.xyz | pixelIndex
+    float4* B;   // direction.xyz | remainingBounces
+    float4* C;   // throughput.rgb | unused
+};
+
+PT_DEV PathReg load_path(const PathBuf& b, int i) {
+    float4 a = b.A[i], d = b.B[i], c = b.C[i];
+    PathReg p;
+    p.o = mk(a.x, a.y, a.z);
+    p.pix = __float_as_int(a.w);
+    p.d = mk(d.x, d.y, d.z);
+    p.rb = __float_as_int(d.w);
+    p.c = mk(c.x, c.y, c.z);
+    return p;
+}
+PT_DEV void store_path(const PathBuf& b, int i, const PathReg& p) {
+    b.A[i] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+    b.B[i] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+    b.C[i] = make_float4(p.c.x, p.c.y, p.c.z, 0.0f);
+}
+
+// local path id of this process -> global pixel index (PIXELS shard: interleaved row bands)
+PT_DEV int shard_pixel(const SceneDev& sc, int l) {
+    if (sc.shard.mode != 1) return l;
+    int W = sc.cam.resx;
+    int lr = l / W, x = l - lr * W;
+    int band = lr / sc.shard.rows, within = lr - band * sc.shard.rows;
+    int y = (band * sc.shard.count + sc.shard.rank) * sc.shard.rows + within;
+    return x + y * W;
+}
+
+// generateRayFromCamera + sampleAperture (pathtrace.cu:231-292) for pixel `index`
+PT_DEV PathReg camera_ray(const CamDev& cam, int iter, int trace_depth, int index) {
+    int y = index / cam.resx;
+    int x = index - y * cam.resx;
+    Rng rng = rng_make(iter, index, 0);
+    float jitterX = u01(rng);
+    float jitterY = u01(rng);
+    float sx = (float)x + jitterX - (float)cam.resx * 0.5f;
+    float sy = (float)y + jitterY - (float)cam.resy * 0.5f;
+    f3 pixelPoint = cam.view - (cam.right * cam.plx) * sx - (cam.up * cam.ply) * sy;
+    f3 rayDir = normalize(pixelPoint);
+    f3 focalPoint = cam.position + rayDir * cam.focalDist;
+    float r = cam.aperture * __builtin_sqrtf(u01(rng));
+    float theta = 2.0f * PI * u01(rng);
+    float s, c;
+    pt_sincosf(theta, &s, &c);
+    f3 apertureOffset = mk(r * c, r * s, 0.0f);
+    PathReg p;
+    p.o = cam.position + apertureOffset;
+    p.c = mk(1.f, 1.f, 1.f);
+    p.d = normalize(focalPoint - p.o);
+    p.pix = index;
+    p.rb = trace_depth;
+    return p;
+}
+
+struct Hit {
+    float t;        // -1 on miss
+    f3 n;
+    int mat;
+    int tri;        // winning triangle (reference index) or -1
+    float u, v;
+};
+
+// bvhMeshIntersectionTest (intersections.cu:148-234): same DFS order (push left, push right,
+// pop right first), same strict `t < t_hit` acceptance, so exact-t ties resolve identically.
+// `stack` is this thread's column of an LDS array (stride BLOCK).  Returns the winner's leaf
+// slot (index into the leaf-ordered hot triangle array) in `btri`.
+PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& bu, float& bv, int& btri) {
+    float t_hit = FLT_MAX_;
+    bool hit = false;
+    btri = -1;
+    int sp = 0;
+    stack[0] = 0;
+    sp = 1;
+    while (sp > 0) {
+        int ni = stack[(--sp) * BLOCK];
+        DevNode nd = sc.nodes[ni];
+        if (!aabb_test(nd.lo, nd.hi, ro, rd)) continue;
+        int a = __float_as_int(nd.lo.w), b = __float_as_int(nd.hi.w);
+        if (b <= -2) {
+            int cnt = -b - 2;
+            for (int i = 0; i < cnt; ++i) {
+                DevTriHot th = sc.hot[a + i];
+                f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+                f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+                f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+                float t, u, v;
+                if (tri_test(ro, rd, v0, v1, v2, t, u, v)) {
+                    if (t < t_hit && t > 0.0f) {
+                        hit = true;
+                        t_hit = t;
+                        bu = u;
+                        bv = v;
+                        btri = a + i;
+                    }
+                }
+            }
+        } else {
+            if (a >= 0 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = a;
+            if (b >= 0 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = b;
+        }
+    }
+    return hit ? t_hit : -1.f;
+}
+
+// computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
+// decides the winner (t and the normal "seed"); the world normal is derived once for the
+// winner — the same value the reference computes for every candidate and then keeps.
+template <bool HAS_BVH>
+PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
+    float t_min = FLT_MAX_;
+    int win = -1;
+    f3 seed = mk(0.f, 0.f, 0.f);
+    for (int i = 0; i < sc.num_geoms; ++i) {
+        const DevGeom& g = sc.geoms[i];
+        f3 s;
+        float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
+        if (t > 0.0f && t_min > t) {
+            t_min = t;
+            win = i;
+            seed = s;
+        }
+    }
+    Hit h;
+    h.tri = -1;
+    h.u = 0.f;
+    h.v = 0.f;
+    f3 normal = mk(0.f, 0.f, 0.f);
+    int hit_index = -1;   // reference hit_geom_index: prim -> its materialid, mesh -> -2
+    int mat = 0;
+    if (win >= 0) {
+        const DevGeom& g = sc.geoms[win];
+        normal = normalize(xform(g.itr, seed, 0.0f));
+        hit_index = g.materialid;
+        mat = g.materialid;
+    }
+    if (HAS_BVH) {
+        if (sc.use_bvh && sc.num_nodes > 0) {
+            float u, v;
+            int tri;
+            float tb = bvh_intersect(sc, ro, rd, stack, u, v, tri);
+            if (tb > 0.0f && tb < t_min) {
+                t_min = tb;
+                hit_index = -2;
+                DevTriHot th = sc.hot[tri];          // bvh_intersect returns the leaf slot
+                int tri_index = __float_as_int(th.c.y);
+                const DevTriCold& cd = sc.cold[tri_index];
+                mat = cd.materialID;
+                h.tri = tri_index;
+                h.u = u;
+                h.v = v;
+                f3 n0 = mk(cd.n0[0], cd.n0[1], cd.n0[2]);
+                f3 n1 = mk(cd.n1[0], cd.n1[1], cd.n1[2]);
+                f3 n2 = mk(cd.n2[0], cd.n2[1], cd.n2[2]);
+                if (length(n0) < 1e-6f || length(n1) < 1e-6f || length(n2) < 1e-6f) {
+                    f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+                    f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+                    f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+                    normal = normalize(cross(v1 - v0, v2 - v0));
+                } else {
+                    float w0 = 1.0f - u - v;
+                    normal = normalize((w0 * n0 + u * n1) + v * n2);
+                }
+            }
+        }
+    }
+    if (hit_index == -1) {
+        h.t = -1.0f;
+        h.n = mk(0.f, 0.f, 0.f);
+        h.mat = 0;
+        return h;
+    }
+    if (dot(rd, normal) > 0.0f) normal = -normal;
+    h.t = t_min;
+    h.n = normal;
+    h.mat = mat;
+    return h;
+}
+
+// kernShadeMaterialProper for one live path (pathtrace.cu:521-621).  Textures: a material
+// that names one with no loaded texture gets sampleTexture's magenta (pathtrace.cu:505-512).
+PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter) {
+    if (h.t > 0.0f) {
+        const DevMaterial m = sc.mats[h.mat];
+        f3 mcolor = m.hasTexture ? mk(1.0f, 0.0f, 1.0f) : mk(m.color[0], m.color[1], m.color[2]);
+        if (m.emittance > 0.0f) {
+            p.c = p.c * (mcolor * m.emittance);
+            p.rb = 0;
+        } else {
+            Rng rng = rng_make(iter, p.pix, p.rb);
+            f3 intersect = p.o + p.d * h.t;
+            scatter(p, intersect, h.n, m, mcolor, rng, sc.arg_order);
+        }
+    } else {
+        p.c = mk(0.0f, 0.0f, 0.0f);
+        p.rb = 0;
+    }
+}
+
+}  // namespace ptd

@@ -1,0 +1,1249 @@
+// pt_runtime.hip — the wavefront path tracer on MI355X: kernels, device buffers, frame loop
+// and the C-ABI of include/pt/pathtrace_abi.h.
+//
+// Two pipelines render bit-identical images (the same per-path functions, pt_kernels.h):
+//
+//  FUSED (default): one kernel per bounce.  Bounce 0 generates the camera ray in registers;
+//    every bounce intersects, shades, adds terminated paths into the image (the reference's
+//    finalGather, done at termination — one add per pixel per frame either way) and compacts
+//    survivors with a wave ballot + LDS block scan + one atomic per block into one of NSEG
+//    output segments (segment = blockIdx % 8, i.e. one per XCD group) — no host round trip,
+//    no per-bounce readback of the live count.
+//
+//  STAGED: one kernel per reference stage — camera, intersect, [material sort], shade,
+//    compaction — each a separately testable HIP kernel.  Its compaction is a STABLE
+//    single-pass partition (wave ballot/mbcnt block scan + decoupled look-back across tiles),
+//    the drop-in for thrust::stable_partition(PathAlive) (pathtrace.cu:750-757).
+//
+// A frame is captured once into a hipGraph and replayed; the iteration number lives in
+// device memory (k_frame_begin advances it), so the replay needs no parameter updates.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pt/pathtrace_abi.h"
+#include "pt_kernels.h"
+
+using namespace ptd;
+
+// =============================================================================================
+// kernels
+// =============================================================================================
+
+// Fold the previous frame's live counts into the running totals, advance (or set) the
+// iteration and zero the per-frame counters.  One block.
+__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels) {
+    int t = threadIdx.x;
+    if (ctl->frames > 0) {
+        for (int b = t; b < MAXB + 1; b += blockDim.x) {
+            unsigned long long s = 0;
+            for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k];
+            ctl->tot[b] += s;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < (MAXB + 1) * NSEG; i += blockDim.x) (&ctl->cnt[0][0])[i] = 0;
+    for (int i = t; i < MAXB; i += blockDim.x) ctl->ticket[i] = 0;
+    __syncthreads();
+    if (t == 0) {
+        ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
+        ctl->cnt[0][0] = local_pixels;
+        ctl->frames += 1;
+    }
+}
+
+PT_DEV uint64_t lanemask_lt() {
+    uint32_t lane = threadIdx.x & 63u;
+    return lane == 0 ? 0ull : (~0ull >> (64u - lane));
+}
+PT_DEV int mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+PT_DEV void gather_into_image(float* image, const PathReg& p) {
+    float* px = image + 3 * (size_t)p.pix;
+    px[0] += p.c.x;
+    px[1] += p.c.y;
+    px[2] += p.c.z;
+}
+
+// --------------------------------------------------------------------------------------------
+// FUSED: camera (bounce 0) | load -> intersect -> shade -> gather dead -> compact survivors
+// --------------------------------------------------------------------------------------------
+template <bool FIRST, bool HAS_BVH>
+__global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
+                                                  float* __restrict__ image, int bounce, int seg_stride) {
+    extern __shared__ int s_stack[];   // HAS_BVH: stack_depth x BLOCK ints
+    __shared__ int s_wave[BLOCK / 64];
+    __shared__ int s_base;
+    const int iter = ctl->iter;
+    int n;
+    int segoff[NSEG + 1];
+    if (FIRST) {
+        n = sc.shard.local_pixels;
+    } else {
+        segoff[0] = 0;
+#pragma unroll
+        for (int s = 0; s < NSEG; ++s) segoff[s + 1] = segoff[s] + ctl->cnt[bounce][s];
+        n = segoff[NSEG];
+    }
+    const int block_start = blockIdx.x * BLOCK;
+    if (block_start >= n) return;
+    const int tid = threadIdx.x;
+    const int gid = block_start + tid;
+    const bool active = gid < n;
+    PathReg p;
+    p.rb = 0;
+    if (active) {
+        if (FIRST) {
+            p = camera_ray(sc.cam, iter, sc.trace_depth, shard_pixel(sc, gid));
+        } else {
+            int s = 0;
+#pragma unroll
+            for (int k = 1; k < NSEG; ++k) s += (gid >= segoff[k]) ? 1 : 0;
+            p = load_path(in, s * seg_stride + (gid - segoff[s]));
+        }
+        if (p.rb > 0) {
+            Hit h = intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
+            shade_path(sc, p, h, iter);
+        }
+    }
+    const bool surv = active && p.rb > 0;
+    if (active && !surv) gather_into_image(image, p);
+
+    // block-aggregated compaction: ballot -> per-wave counts -> one atomic per block
+    const uint64_t m = __ballot(surv);
+    const int lane = tid & 63, w = tid >> 6;
+    if (lane == 0) s_wave[w] = __popcll(m);
+    __syncthreads();
+    if (tid == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) {
+            int c = s_wave[i];
+            s_wave[i] = tot;
+            tot += c;
+        }
+        const int seg = blockIdx.x & (NSEG - 1);
+        s_base = tot ? seg * seg_stride + atomicAdd(&ctl->cnt[bounce + 1][seg], tot) : 0;
+    }
+    __syncthreads();
+    if (surv) store_path(out, s_base + s_wave[w] + mbcnt(m), p);
+}
+
+// --------------------------------------------------------------------------------------------
+// STAGED kernels (single contiguous segment)
+// --------------------------------------------------------------------------------------------
+struct HitBuf {
+    float4* nt;     // surfaceNormal.xyz | t
+    int* mat;       // materialId
+};
+
+__global__ __launch_bounds__(BLOCK) void k_camera(SceneDev sc, PathBuf out, FrameCtl* ctl) {
+    int gid = blockIdx.x * BLOCK + threadIdx.x;
+    if (gid >= sc.shard.local_pixels) return;
+    store_path(out, gid, camera_ray(sc.cam, ctl->iter, sc.trace_depth, shard_pixel(sc, gid)));
+}
+
+template <bool HAS_BVH>
+__global__ __launch_bounds__(BLOCK) void k_intersect(SceneDev sc, PathBuf in, HitBuf hits, const int* n_ptr) {
+    extern __shared__ int s_stack[];
+    const int n = *n_ptr;
+    int gid = blockIdx.x * BLOCK + threadIdx.x;
+    if (blockIdx.x * BLOCK >= n || gid >= n) return;
+    float4 a = in.A[gid], b = in.B[gid];
+    Hit h = intersect_scene<HAS_BVH>(sc, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), s_stack + threadIdx.x);
+    hits.nt[gid] = make_float4(h.n.x, h.n.y, h.n.z, h.t);
+    hits.mat[gid] = h.mat;
+}
+
+// shade (optionally through a material-sorted permutation); terminated paths are gathered
+// into the image unless image == nullptr; alive flags feed the compaction kernel.
+__global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBuf hits, const int* perm,
+                                                 const int* n_ptr, const FrameCtl* ctl, int iter_override,
+                                                 float* image, int* alive) {
+    const int n = *n_ptr;
+    int j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    int i = perm ? perm[j] : j;
+    PathReg p = load_path(buf, i);
+    if (p.rb <= 0) {                 // pathtrace.cu:535-537
+        if (alive) alive[i] = 0;
+        return;
+    }
+    float4 nt = hits.nt[i];
+    Hit h;
+    h.t = nt.w;
+    h.n = mk(nt.x, nt.y, nt.z);
+    h.mat = hits.mat[i];
+    h.tri = -1;
+    h.u = h.v = 0.f;
+    const int iter = iter_override > 0 ? iter_override : ctl->iter;
+    shade_path(sc, p, h, iter);
+    store_path(buf, i, p);
+    if (p.rb <= 0 && image) gather_into_image(image, p);
+    if (alive) alive[i] = p.rb > 0;
+}
+
+// ---- stable compaction: tile-local ballot scan + decoupled look-back ----
+constexpr int CITEMS = 8;                       // items per thread
+constexpr int CTILE = BLOCK * CITEMS;           // 2048 items per tile
+constexpr uint64_t ST_AGG = 1ull << 32, ST_INC = 2ull << 32;
+
+PT_DEV uint64_t st_load(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+PT_DEV void st_store(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// status word: [63:40] epoch  [39:32] flag (1 aggregate, 2 inclusive)  [31:0] count
+__global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, const int* __restrict__ alive,
+                                                   const int* n_ptr, int* n_out, int* ticket,
+                                                   uint64_t* status, uint32_t epoch) {
+    __shared__ int s_cnt[CITEMS][BLOCK / 64];
+    __shared__ int s_tile;
+    __shared__ int s_prefix;
+    const int n = *n_ptr;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    const int base = tile * CTILE;
+    if (base >= n) return;
+    bool f[CITEMS];
+    uint64_t m[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) {
+        int idx = base + k * BLOCK + tid;
+        f[k] = idx < n && alive[idx] != 0;
+        m[k] = __ballot(f[k]);
+        if (lane == 0) s_cnt[k][w] = __popcll(m[k]);
+    }
+    __syncthreads();
+    // tile aggregate and per-(k, wave) exclusive offsets, in item order (k-major, then wave)
+    if (tid == 0) {
+        int run = 0;
+        for (int k = 0; k < CITEMS; ++k)
+            for (int i = 0; i < BLOCK / 64; ++i) {
+                int c = s_cnt[k][i];
+                s_cnt[k][i] = run;
+                run += c;
+            }
+        const uint64_t tag = (uint64_t)epoch << 40;
+        int excl = 0;
+        if (tile == 0) {
+            st_store(&status[0], tag | ST_INC | (uint32_t)run);
+        } else {
+            st_store(&status[tile], tag | ST_AGG | (uint32_t)run);
+            uint32_t spins = 0;
+            for (int t = tile - 1; t >= 0;) {
+                uint64_t s = st_load(&status[t]);
+                if ((s >> 40) != epoch || ((s >> 32) & 0xff) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) break;   // bounded: never hang the GPU (result then wrong, flagged by tests)
+                    continue;                          // predecessor not published yet
+                }
+                excl += (int)(uint32_t)s;
+                if (((s >> 32) & 0xff) == 2) break;
+                --t;
+            }
+            st_store(&status[tile], tag | ST_INC | (uint32_t)(excl + run));
+        }
+        s_prefix = excl;
+        if (base + CTILE >= n) *n_out = excl + run;   // the last tile publishes the count
+    }
+    __syncthreads();
+    const int prefix = s_prefix;
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) {
+        if (f[k]) {
+            int idx = base + k * BLOCK + tid;
+            int dst = prefix + s_cnt[k][w] + mbcnt(m[k]);
+            out.A[dst] = in.A[idx];
+            out.B[dst] = in.B[idx];
+            out.C[dst] = in.C[idx];
+        }
+    }
+}
+
+// ---- stable counting sort of materialId (MATERIAL_SORTING, pathtrace.cu:730-735) ----
+constexpr int MAXMAT = 256;
+
+// per-tile key histogram, tile = CTILE items
+__global__ __launch_bounds__(BLOCK) void k_sort_hist(const int* __restrict__ keys, const int* n_ptr, int nkeys,
+                                                     int* tile_hist) {
+    __shared__ int h[MAXMAT];
+    const int n = *n_ptr;
+    const int tile = blockIdx.x, base = tile * CTILE;
+    for (int i = threadIdx.x; i < nkeys; i += BLOCK) h[i] = 0;
+    __syncthreads();
+    if (base < n) {
+        for (int k = 0; k < CITEMS; ++k) {
+            int idx = base + k * BLOCK + threadIdx.x;
+            if (idx < n) atomicAdd(&h[keys[idx]], 1);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nkeys; i += BLOCK) tile_hist[(size_t)tile * nkeys + i] = h[i];
+}
+
+// exclusive scan over (key, tile) in key-major order; one block
+__global__ __launch_bounds__(BLOCK) void k_sort_scan(int* tile_hist, const int* n_ptr, int nkeys) {
+    const int n = *n_ptr;
+    const int ntiles = (n + CTILE - 1) / CTILE;
+    __shared__ int key_tot[MAXMAT];
+    __shared__ int key_off[MAXMAT];
+    for (int key = threadIdx.x; key < nkeys; key += BLOCK) {
+        int s = 0;
+        for (int t = 0; t < ntiles; ++t) {
+            int c = tile_hist[(size_t)t * nkeys + key];
+            tile_hist[(size_t)t * nkeys + key] = s;
+            s += c;
+        }
+        key_tot[key] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int k = 0; k < nkeys; ++k) { key_off[k] = run; run += key_tot[k]; }
+    }
+    __syncthreads();
+    for (int key = threadIdx.x; key < nkeys; key += BLOCK)
+        for (int t = 0; t < ntiles; ++t) tile_hist[(size_t)t * nkeys + key] += key_off[key];
+}
+
+// stable scatter: rank among equal keys = earlier items of the tile (item order k-major, wave,
+// lane) — peers found with one ballot per key bit
+__global__ __launch_bounds__(BLOCK) void k_sort_scatter(const int* __restrict__ keys, const int* n_ptr, int nkeys,
+                                                        int key_bits, const int* tile_off, int* perm) {
+    __shared__ int run[MAXMAT];           // items of each key already placed in this tile
+    __shared__ int wcnt[BLOCK / 64][MAXMAT];
+    const int n = *n_ptr;
+    const int tile = blockIdx.x, base = tile * CTILE;
+    if (base >= n) return;
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < nkeys; i += BLOCK) run[i] = 0;
+    __syncthreads();
+    for (int k = 0; k < CITEMS; ++k) {
+        int idx = base + k * BLOCK + tid;
+        bool valid = idx < n;
+        int key = valid ? keys[idx] : 0;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < key_bits; ++b) {
+            uint64_t bb = __ballot(valid && ((key >> b) & 1));
+            peers &= ((key >> b) & 1) ? bb : ~bb;
+        }
+        for (int i = tid; i < (BLOCK / 64) * MAXMAT; i += BLOCK) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        // the lowest lane of each peer group publishes the group size for its wave
+        if (valid && mbcnt(peers) == 0) wcnt[w][key] = __popcll(peers);
+        __syncthreads();
+        if (valid) {
+            int r = run[key] + mbcnt(peers);
+            for (int ww = 0; ww < w; ++ww) r += wcnt[ww][key];
+            perm[tile_off[(size_t)tile * nkeys + key] + r] = idx;
+        }
+        __syncthreads();
+        for (int key2 = tid; key2 < nkeys; key2 += BLOCK) {
+            int s = 0;
+            for (int ww = 0; ww < BLOCK / 64; ++ww) s += wcnt[ww][key2];
+            run[key2] += s;
+        }
+        __syncthreads();
+    }
+}
+
+// sendImageToPBO (pathtrace.cu:59-80)
+__global__ void k_to_pbo(const float* __restrict__ image, pt_uchar4* pbo, int n, int iter) {
+    int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    int c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double d = (double)(image[3 * (size_t)i + k] / (float)iter) * 255.0;
+        int v = (d != d) ? 0 : (d >= 2147483647.0 ? 2147483647 : (d <= -2147483648.0 ? (-2147483647 - 1) : (int)d));
+        c[k] = v < 0 ? 0 : (v > 255 ? 255 : v);
+    }
+    pt_uchar4 o;
+    o.x = (uint8_t)c[0];
+    o.y = (uint8_t)c[1];
+    o.z = (uint8_t)c[2];
+    o.w = 0;
+    pbo[i] = o;
+}
+
+__global__ void k_rng(const int* iid, int m, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    Rng r = rng_make(iid[3 * i], iid[3 * i + 1], iid[3 * i + 2]);
+    for (int k = 0; k < n; ++k) out[(size_t)i * n + k] = u01(r);
+}
+
+// =============================================================================================
+// host runtime
+// =============================================================================================
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(PT_E_HIP, "%s:%d: %s: %s", __FILE__, __LINE__, #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return PT_OK;
+    HIPCHK(hipMalloc((void**)p, n * sizeof(T)));
+    return PT_OK;
+}
+
+struct State {
+    bool inited = false;
+    pt_options opts{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    SceneDev sc{};
+    int width = 0, height = 0, pixels_total = 0, local_pixels = 0;
+    int seg_stride = 0, capacity = 0;
+    bool has_bvh = false;
+    int stack_depth = 0;
+    size_t bvh_lds = 0;
+    // device buffers
+    DevGeom* d_geoms = nullptr;
+    DevMaterial* d_mats = nullptr;
+    DevNode* d_nodes = nullptr;
+    DevTriHot* d_hot = nullptr;
+    DevTriCold* d_cold = nullptr;
+    float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    float4* d_hit_nt = nullptr;
+    int* d_hit_mat = nullptr;
+    int* d_alive = nullptr;
+    int* d_perm = nullptr;
+    int* d_tile_hist = nullptr;
+    uint64_t* d_status = nullptr;
+    float* d_image = nullptr;
+    FrameCtl* d_ctl = nullptr;
+    // graph
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    int last_iter = 0;
+    int frames_done = 0;
+    int32_t* traced_depth = nullptr;
+    int key_bits = 1;
+};
+State g;
+
+PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path[i][2]}; }
+int nblocks(int n) { return (n + BLOCK - 1) / BLOCK; }
+
+void release_graph() {
+    if (g.graph_exec) (void)hipGraphExecDestroy(g.graph_exec);
+    if (g.graph) (void)hipGraphDestroy(g.graph);
+    g.graph_exec = nullptr;
+    g.graph = nullptr;
+}
+
+// device-side counter of the input of bounce b in the staged pipeline
+const int* staged_count(int b) { return &g.d_ctl->cnt[b][0]; }
+
+// Enqueue one frame's kernels (everything after k_frame_begin) on g.stream.  `ev` (optional):
+// events recorded before the first and after every kernel, for pt_profile_frames.
+int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
+    const int depth = g.sc.trace_depth;
+    const int nb = nblocks(g.local_pixels);
+    auto mark = [&](int kind) {
+        if (ev) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            (void)hipEventRecord(e, g.stream);
+            ev->push_back(e);
+            ev_kind->push_back(kind);
+        }
+    };
+    mark(-1);
+    const int nbounces = std::max(1, depth);
+    if (g.opts.pipeline == PT_PIPELINE_FUSED) {
+        for (int b = 0; b < nbounces; ++b) {
+            PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
+            size_t lds = g.has_bvh ? g.bvh_lds : 0;
+            if (b == 0) {
+                if (g.has_bvh)
+                    hipLaunchKernelGGL((k_bounce<true, true>), dim3(nb), dim3(BLOCK), lds, g.stream, g.sc, in, out,
+                                       g.d_ctl, g.d_image, b, g.seg_stride);
+                else
+                    hipLaunchKernelGGL((k_bounce<true, false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, in, out,
+                                       g.d_ctl, g.d_image, b, g.seg_stride);
+            } else {
+                if (g.has_bvh)
+                    hipLaunchKernelGGL((k_bounce<false, true>), dim3(nb), dim3(BLOCK), lds, g.stream, g.sc, in, out,
+                                       g.d_ctl, g.d_image, b, g.seg_stride);
+                else
+                    hipLaunchKernelGGL((k_bounce<false, false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, in, out,
+                                       g.d_ctl, g.d_image, b, g.seg_stride);
+            }
+            HIPCHK(hipGetLastError());
+            mark(100 + b);
+        }
+        return PT_OK;
+    }
+    // STAGED
+    hipLaunchKernelGGL(k_camera, dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
+    HIPCHK(hipGetLastError());
+    mark(0);
+    const int ntiles = (g.local_pixels + CTILE - 1) / CTILE;
+    int cur = 0;
+    for (int b = 0; b < nbounces; ++b) {
+        // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
+        const int* n_in = g.opts.stream_compaction ? staged_count(b) : staged_count(0);
+        HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+        if (g.has_bvh)
+            hipLaunchKernelGGL((k_intersect<true>), dim3(nb), dim3(BLOCK), g.bvh_lds, g.stream, g.sc, pathbuf(cur),
+                               hits, n_in);
+        else
+            hipLaunchKernelGGL((k_intersect<false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(cur), hits,
+                               n_in);
+        HIPCHK(hipGetLastError());
+        mark(1);
+        const int* perm = nullptr;
+        if (g.opts.material_sort) {
+            const int nk = std::max(1, g.sc.num_mats);
+            hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
+                               g.d_tile_hist);
+            hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, n_in, nk);
+            hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
+                               g.key_bits, g.d_tile_hist, g.d_perm);
+            HIPCHK(hipGetLastError());
+            perm = g.d_perm;
+            mark(4);
+        }
+        hipLaunchKernelGGL(k_shade, dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(cur), hits, perm, n_in,
+                           (const FrameCtl*)g.d_ctl, 0, g.d_image, g.opts.stream_compaction ? g.d_alive : nullptr);
+        HIPCHK(hipGetLastError());
+        mark(2);
+        if (g.opts.stream_compaction) {
+            uint32_t epoch = (uint32_t)((g.frames_done * 64 + b + 1) & 0xffffff);
+            // epoch in a captured graph is frozen; replays reset the status words instead
+            hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(cur), pathbuf(cur ^ 1),
+                               (const int*)g.d_alive, n_in, &g.d_ctl->cnt[b + 1][0], &g.d_ctl->ticket[b], g.d_status,
+                               epoch);
+            HIPCHK(hipGetLastError());
+            mark(3);
+            cur ^= 1;
+        }
+    }
+    return PT_OK;
+}
+
+int enqueue_frame(int set_iter, std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, set_iter, g.local_pixels);
+    HIPCHK(hipGetLastError());
+    if (g.opts.pipeline == PT_PIPELINE_STAGED && g.opts.stream_compaction) {
+        // look-back status words must not carry a previous frame's INCLUSIVE flag of the same epoch
+        HIPCHK(hipMemsetAsync(g.d_status, 0, sizeof(uint64_t) * (size_t)((g.capacity + CTILE - 1) / CTILE + 1),
+                              g.stream));
+    }
+    return enqueue_frame_body(ev, ev_kind);
+}
+
+int build_graph() {
+    release_graph();
+    HIPCHK(hipStreamBeginCapture(g.stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_frame(0, nullptr, nullptr);
+    hipGraph_t gr = nullptr;
+    hipError_t e = hipStreamEndCapture(g.stream, &gr);
+    if (rc != PT_OK) return rc;
+    HIPCHK(e);
+    g.graph = gr;
+    HIPCHK(hipGraphInstantiate(&g.graph_exec, g.graph, nullptr, nullptr, 0));
+    return PT_OK;
+}
+
+// one frame with iteration `iter`
+int run_frame(int iter) {
+    if (g.opts.use_graph) {
+        if (!g.graph_exec) {
+            int rc = build_graph();
+            if (rc != PT_OK) return rc;
+        }
+        // the graph's k_frame_begin increments: preset iter - 1 (stream-ordered)
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&g.d_ctl->iter, iter - 1, 1, g.stream));
+        HIPCHK(hipGraphLaunch(g.graph_exec, g.stream));
+    } else {
+        int rc = enqueue_frame(iter, nullptr, nullptr);
+        if (rc != PT_OK) return rc;
+    }
+    g.last_iter = iter;
+    g.frames_done++;
+    return PT_OK;
+}
+
+// max DFS stack the reference traversal can reach on this tree (no culling)
+int bvh_max_stack(const pt_bvh_node* nodes, int n) {
+    if (n <= 0) return 0;
+    std::vector<int> st;
+    st.push_back(0);
+    size_t mx = 1;
+    std::vector<char> seen(n, 0);
+    while (!st.empty()) {
+        int i = st.back();
+        st.pop_back();
+        if (i < 0 || i >= n || seen[i]) continue;
+        seen[i] = 1;
+        const pt_bvh_node& nd = nodes[i];
+        if (nd.triCount > 0 && nd.start >= 0) continue;
+        if (nd.left >= 0) st.push_back(nd.left);
+        if (nd.right >= 0) st.push_back(nd.right);
+        mx = std::max(mx, st.size());
+    }
+    return (int)mx;
+}
+
+void free_all() {
+    release_graph();
+    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_alive,
+                    g.d_perm, g.d_tile_hist, g.d_status, g.d_image, g.d_ctl};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k)
+            if (g.d_path[i][k]) (void)hipFree(g.d_path[i][k]);
+    if (g.stream) (void)hipStreamDestroy(g.stream);
+    int32_t* td = g.traced_depth;
+    g = State();
+    g.traced_depth = td;
+}
+
+template <class T>
+int upload(T* d, const T* h, size_t n) {
+    if (n) HIPCHK(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+CamDev to_camdev(const pt_camera& c) {
+    CamDev d;
+    d.resx = c.resolution.x;
+    d.resy = c.resolution.y;
+    d.position = f3{c.position.x, c.position.y, c.position.z};
+    d.view = f3{c.view.x, c.view.y, c.view.z};
+    d.up = f3{c.up.x, c.up.y, c.up.z};
+    d.right = f3{c.right.x, c.right.y, c.right.z};
+    d.plx = c.pixelLength.x;
+    d.ply = c.pixelLength.y;
+    d.aperture = c.aperture;
+    d.focalDist = c.focalDist;
+    return d;
+}
+
+// AoS (reference layout) <-> SoA wavefront
+void paths_to_soa(const pt_path_segment* p, int64_t n, std::vector<float4>& A, std::vector<float4>& B,
+                  std::vector<float4>& C) {
+    A.resize(n);
+    B.resize(n);
+    C.resize(n);
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t pix = p[i].pixelIndex, rb = p[i].remainingBounces;
+        float fp, fr;
+        memcpy(&fp, &pix, 4);
+        memcpy(&fr, &rb, 4);
+        A[i] = make_float4(p[i].ray.origin.x, p[i].ray.origin.y, p[i].ray.origin.z, fp);
+        B[i] = make_float4(p[i].ray.direction.x, p[i].ray.direction.y, p[i].ray.direction.z, fr);
+        C[i] = make_float4(p[i].color.x, p[i].color.y, p[i].color.z, 0.f);
+    }
+}
+void soa_to_paths(const std::vector<float4>& A, const std::vector<float4>& B, const std::vector<float4>& C,
+                  int64_t n, pt_path_segment* p) {
+    for (int64_t i = 0; i < n; ++i) {
+        p[i].ray.origin = pt_vec3{A[i].x, A[i].y, A[i].z};
+        p[i].ray.direction = pt_vec3{B[i].x, B[i].y, B[i].z};
+        p[i].color = pt_vec3{C[i].x, C[i].y, C[i].z};
+        memcpy(&p[i].pixelIndex, &A[i].w, 4);
+        memcpy(&p[i].remainingBounces, &B[i].w, 4);
+    }
+}
+
+int upload_paths(int buf, const pt_path_segment* paths, int64_t n) {
+    std::vector<float4> A, B, C;
+    paths_to_soa(paths, n, A, B, C);
+    HIPCHK(hipMemcpy(g.d_path[buf][0], A.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.d_path[buf][1], B.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.d_path[buf][2], C.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+int download_paths(int buf, int64_t n, pt_path_segment* out) {
+    std::vector<float4> A(n), B(n), C(n);
+    HIPCHK(hipMemcpy(A.data(), g.d_path[buf][0], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(B.data(), g.d_path[buf][1], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(C.data(), g.d_path[buf][2], n * sizeof(float4), hipMemcpyDeviceToHost));
+    soa_to_paths(A, B, C, n, out);
+    return PT_OK;
+}
+int set_count(int slot, int value) {
+    HIPCHK(hipMemcpy(&g.d_ctl->cnt[slot][0], &value, sizeof(int), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+#define RC(x)                      \
+    do {                           \
+        int rc_ = (x);             \
+        if (rc_ != PT_OK) return rc_; \
+    } while (0)
+
+int need_init() { return g.inited ? PT_OK : fail(PT_E_STATE, "pt_init has not been called"); }
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+int32_t pt_abi_version(void) { return PT_ABI_VERSION; }
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+void pt_default_options(pt_options* o) {
+    memset(o, 0, sizeof(*o));
+    o->stream_compaction = 1;
+    o->material_sort = 0;
+    o->bvh = 1;
+    o->arg_order = 0;
+    o->pipeline = PT_PIPELINE_FUSED;
+    o->use_graph = 1;
+    o->device = 0;
+    o->shard_mode = PT_SHARD_NONE;
+    o->shard_rank = 0;
+    o->shard_count = 1;
+    o->shard_rows = 8;
+    o->block_size = BLOCK;
+}
+
+int32_t pt_init_data_container(int32_t* traced_depth) {
+    g.traced_depth = traced_depth;
+    return PT_OK;
+}
+
+int32_t pt_free(void) {
+    if (g.inited) free_all();
+    g.inited = false;
+    return PT_OK;
+}
+
+int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
+    if (!s) return fail(PT_E_INVALID, "scene is NULL");
+    pt_free();
+    pt_options o;
+    if (opts_in) o = *opts_in;
+    else pt_default_options(&o);
+    if (o.block_size != BLOCK) return fail(PT_E_UNSUPPORTED, "block_size must be %d", BLOCK);
+    const int W = s->camera.resolution.x, H = s->camera.resolution.y;
+    if (W <= 0 || H <= 0) return fail(PT_E_INVALID, "bad resolution %dx%d", W, H);
+    if (s->trace_depth > MAXB) return fail(PT_E_UNSUPPORTED, "trace depth %d > %d", s->trace_depth, MAXB);
+    if (s->num_geoms < 0 || s->num_materials < 0 || s->num_triangles < 0 || s->num_bvh_nodes < 0)
+        return fail(PT_E_INVALID, "negative counts");
+    if (s->num_materials > MAXMAT) return fail(PT_E_UNSUPPORTED, "more than %d materials", MAXMAT);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
+    if (o.device < 0 || o.device >= ndev) return fail(PT_E_INVALID, "device %d out of range", o.device);
+    HIPCHK(hipSetDevice(o.device));
+    g.opts = o;
+    g.device = o.device;
+    HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    g.width = W;
+    g.height = H;
+    g.pixels_total = W * H;
+    // shard
+    ShardDev sh{};
+    sh.mode = o.shard_mode == PT_SHARD_PIXELS && o.shard_count > 1 ? 1 : 0;
+    sh.rank = o.shard_rank;
+    sh.count = std::max(1, o.shard_count);
+    sh.rows = std::max(1, o.shard_rows);
+    if (sh.mode == 1) {
+        if (o.shard_rank < 0 || o.shard_rank >= o.shard_count) return fail(PT_E_INVALID, "bad shard rank");
+        int rows = 0;
+        for (int y = 0; y < H; ++y) rows += ((y / sh.rows) % sh.count) == sh.rank;
+        sh.local_pixels = rows * W;
+    } else {
+        sh.local_pixels = g.pixels_total;
+    }
+    g.local_pixels = sh.local_pixels;
+    const int nb = nblocks(std::max(1, g.local_pixels));
+    g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK;
+    g.capacity = std::max(g.seg_stride * NSEG, ((g.local_pixels + CTILE - 1) / CTILE) * CTILE);
+
+    // ---- scene -> device records ----
+    std::vector<DevGeom> geoms(s->num_geoms);
+    for (int i = 0; i < s->num_geoms; ++i) {
+        const pt_geom& gg = s->geoms[i];
+        DevGeom& d = geoms[i];
+        memset(&d, 0, sizeof d);
+        for (int c = 0; c < 4; ++c)
+            for (int r = 0; r < 3; ++r) {
+                d.inv[c * 3 + r] = gg.inverseTransform.m[c][r];
+                d.fwd[c * 3 + r] = gg.transform.m[c][r];
+                d.itr[c * 3 + r] = gg.invTranspose.m[c][r];
+            }
+        d.type = gg.type;
+        d.materialid = gg.materialid;
+    }
+    std::vector<DevMaterial> mats(std::max(1, s->num_materials));
+    for (int i = 0; i < s->num_materials; ++i) {
+        const pt_material& m = s->materials[i];
+        DevMaterial& d = mats[i];
+        memset(&d, 0, sizeof d);
+        d.color[0] = m.color.x;
+        d.color[1] = m.color.y;
+        d.color[2] = m.color.z;
+        d.emittance = m.emittance;
+        d.hasReflective = m.hasReflective;
+        d.hasRefractive = m.hasRefractive;
+        d.roughness = m.roughness;
+        d.metallic = m.metallic;
+        d.ior = m.indexOfRefraction;
+        d.hasTexture = m.hasTexture ? 1 : 0;
+        d.textureID = m.textureID;
+    }
+    // BVH: only when the reference would traverse it (BVH_ACCELERATION and a non-empty tree)
+    g.has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
+    std::vector<DevNode> nodes;
+    std::vector<DevTriHot> hot;
+    std::vector<DevTriCold> cold;
+    if (g.has_bvh) {
+        nodes.resize(s->num_bvh_nodes);
+        for (int i = 0; i < s->num_bvh_nodes; ++i) {
+            const pt_bvh_node& nd = s->bvh_nodes[i];
+            bool leaf = nd.triCount > 0 && nd.start >= 0;
+            int a = leaf ? nd.start : nd.left;
+            int b = leaf ? -(nd.triCount + 2) : (nd.right >= 0 ? nd.right : -1);
+            if (leaf && (int64_t)nd.start + nd.triCount > s->num_tri_indices)
+                return fail(PT_E_INVALID, "BVH leaf %d indexes past triIndices", i);
+            if (!leaf && (nd.left >= s->num_bvh_nodes || nd.right >= s->num_bvh_nodes))
+                return fail(PT_E_INVALID, "BVH node %d child out of range", i);
+            float fa, fb;
+            memcpy(&fa, &a, 4);
+            memcpy(&fb, &b, 4);
+            nodes[i].lo = make_float4(nd.aabb.min.x, nd.aabb.min.y, nd.aabb.min.z, fa);
+            nodes[i].hi = make_float4(nd.aabb.max.x, nd.aabb.max.y, nd.aabb.max.z, fb);
+        }
+        hot.resize(s->num_tri_indices);
+        for (int k = 0; k < s->num_tri_indices; ++k) {
+            int ti = s->tri_indices[k];
+            if (ti < 0 || ti >= s->num_triangles) return fail(PT_E_INVALID, "triIndices[%d] out of range", k);
+            const pt_triangle& t = s->triangles[ti];
+            float fti;
+            memcpy(&fti, &ti, 4);
+            hot[k].a = make_float4(t.v1.position.x, t.v1.position.y, t.v1.position.z, t.v2.position.x);
+            hot[k].b = make_float4(t.v2.position.y, t.v2.position.z, t.v3.position.x, t.v3.position.y);
+            hot[k].c = make_float4(t.v3.position.z, fti, 0.f, 0.f);
+        }
+        cold.resize(s->num_triangles);
+        for (int i = 0; i < s->num_triangles; ++i) {
+            const pt_triangle& t = s->triangles[i];
+            DevTriCold& c = cold[i];
+            memset(&c, 0, sizeof c);
+            const pt_vertex* v[3] = {&t.v1, &t.v2, &t.v3};
+            float* ns[3] = {c.n0, c.n1, c.n2};
+            float* uvs[3] = {c.uv0, c.uv1, c.uv2};
+            for (int k = 0; k < 3; ++k) {
+                ns[k][0] = v[k]->normal.x;
+                ns[k][1] = v[k]->normal.y;
+                ns[k][2] = v[k]->normal.z;
+                uvs[k][0] = v[k]->uv.x;
+                uvs[k][1] = v[k]->uv.y;
+            }
+            c.dpdu[0] = t.dpdu.x; c.dpdu[1] = t.dpdu.y; c.dpdu[2] = t.dpdu.z;
+            c.dpdv[0] = t.dpdv.x; c.dpdv[1] = t.dpdv.y; c.dpdv[2] = t.dpdv.z;
+            c.materialID = t.materialID;
+        }
+        g.stack_depth = std::min(MAXSTACK, std::max(2, bvh_max_stack(s->bvh_nodes, s->num_bvh_nodes)));
+        g.bvh_lds = (size_t)g.stack_depth * BLOCK * sizeof(int);
+    }
+    for (int i = 0; i < s->num_geoms; ++i)
+        if (s->geoms[i].materialid >= std::max(1, s->num_materials))
+            return fail(PT_E_INVALID, "geom %d material %d out of range", i, s->geoms[i].materialid);
+
+    RC(dalloc(&g.d_geoms, geoms.size()));
+    RC(dalloc(&g.d_mats, mats.size()));
+    RC(upload(g.d_geoms, geoms.data(), geoms.size()));
+    RC(upload(g.d_mats, mats.data(), mats.size()));
+    if (g.has_bvh) {
+        RC(dalloc(&g.d_nodes, nodes.size()));
+        RC(dalloc(&g.d_hot, hot.size()));
+        RC(dalloc(&g.d_cold, cold.size()));
+        RC(upload(g.d_nodes, nodes.data(), nodes.size()));
+        RC(upload(g.d_hot, hot.data(), hot.size()));
+        RC(upload(g.d_cold, cold.data(), cold.size()));
+    }
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
+    RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
+    RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
+    RC(dalloc(&g.d_alive, (size_t)g.capacity));
+    RC(dalloc(&g.d_perm, (size_t)g.capacity));
+    const int ntiles = (g.capacity + CTILE - 1) / CTILE + 1;
+    RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, s->num_materials)));
+    RC(dalloc(&g.d_status, (size_t)ntiles));
+    HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * ntiles));
+    RC(dalloc(&g.d_image, (size_t)g.pixels_total * 3));
+    HIPCHK(hipMemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
+    RC(dalloc(&g.d_ctl, 1));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    g.key_bits = 1;
+    while ((1 << g.key_bits) < std::max(2, s->num_materials)) g.key_bits++;
+
+    SceneDev& sc = g.sc;
+    sc.geoms = g.d_geoms;
+    sc.mats = g.d_mats;
+    sc.nodes = g.d_nodes;
+    sc.hot = g.d_hot;
+    sc.cold = g.d_cold;
+    sc.num_geoms = s->num_geoms;
+    sc.num_mats = s->num_materials;
+    sc.num_nodes = g.has_bvh ? s->num_bvh_nodes : 0;
+    sc.num_tris = s->num_triangles;
+    sc.trace_depth = s->trace_depth;
+    sc.arg_order = o.arg_order;
+    sc.use_bvh = g.has_bvh ? 1 : 0;
+    sc.stack_depth = g.stack_depth;
+    sc.cam = to_camdev(s->camera);
+    sc.shard = sh;
+    g.inited = true;
+    HIPCHK(hipDeviceSynchronize());
+    return PT_OK;
+}
+
+int32_t pt_set_camera(const pt_camera* c) {
+    RC(need_init());
+    if (!c || c->resolution.x != g.width || c->resolution.y != g.height)
+        return fail(PT_E_INVALID, "camera resolution must match pt_init");
+    CamDev nc = to_camdev(*c);
+    if (memcmp(&nc, &g.sc.cam, sizeof nc) != 0) {
+        g.sc.cam = nc;
+        release_graph();   // kernel arguments changed
+    }
+    return PT_OK;
+}
+
+int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_image) {
+    (void)frame;   // unused by the reference too (pathtrace.cu:639)
+    RC(need_init());
+    if (iteration <= 0) return fail(PT_E_INVALID, "iteration is 1-based (main.cpp:458), got %d", iteration);
+    RC(run_frame(iteration));
+    if (pbo) {
+        hipLaunchKernelGGL(k_to_pbo, dim3(nblocks(g.pixels_total)), dim3(BLOCK), 0, g.stream, g.d_image, pbo,
+                           g.pixels_total, iteration);
+        HIPCHK(hipGetLastError());
+    }
+    if (host_image)
+        HIPCHK(hipMemcpyAsync(host_image, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total,
+                              hipMemcpyDeviceToHost, g.stream));
+    HIPCHK(hipStreamSynchronize(g.stream));
+    if (g.traced_depth) *g.traced_depth = std::max(1, g.sc.trace_depth);
+    return PT_OK;
+}
+
+int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
+    RC(need_init());
+    if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
+    for (int i = 0; i < count; ++i) RC(run_frame(first_iteration + i));
+    return PT_OK;
+}
+
+int32_t pt_synchronize(void) {
+    RC(need_init());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    return PT_OK;
+}
+
+int32_t pt_get_image(float* host_out, int64_t n_floats) {
+    RC(need_init());
+    if (!host_out || n_floats < (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image buffer too small");
+    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemcpy(host_out, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
+    RC(need_init());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    if (device_ptr) *device_ptr = g.d_image;
+    if (n_floats) *n_floats = (int64_t)g.pixels_total * 3;
+    return PT_OK;
+}
+
+int32_t pt_set_image(const float* host_in, int64_t n_floats) {
+    RC(need_init());
+    if (!host_in || n_floats != (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
+    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemcpy(g.d_image, host_in, sizeof(float) * (size_t)n_floats, hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+int32_t pt_get_frame_stats(pt_frame_stats* out) {
+    RC(need_init());
+    if (!out) return fail(PT_E_INVALID, "NULL");
+    HIPCHK(hipStreamSynchronize(g.stream));
+    FrameCtl ctl;
+    HIPCHK(hipMemcpy(&ctl, g.d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    memset(out, 0, sizeof(*out));
+    out->iteration = ctl.iter;
+    out->bounces = std::max(1, g.sc.trace_depth);
+    out->pixels = g.local_pixels;
+    for (int b = 0; b < out->bounces; ++b) {
+        int64_t s = 0;
+        if (g.opts.pipeline == PT_PIPELINE_STAGED && !g.opts.stream_compaction) {
+            s = b == 0 ? g.local_pixels : -1;   // no compaction: the live count is never formed
+        } else {
+            for (int k = 0; k < NSEG; ++k) s += ctl.cnt[b][k];
+        }
+        out->live[b] = s;
+        if (s > 0) out->segments += s;
+    }
+    out->frames_total = (int64_t)ctl.frames;
+    for (int b = 0; b <= MAXB; ++b) {
+        int64_t cur = 0;
+        for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k];
+        out->live_total[b] = (int64_t)ctl.tot[b] + (ctl.frames > 0 ? cur : 0);
+        if (b < out->bounces) out->segments_total += out->live_total[b];
+    }
+    return PT_OK;
+}
+
+int32_t pt_reset_stats(void) {
+    RC(need_init());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// test entry points
+// ---------------------------------------------------------------------------------------------
+int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
+    RC(need_init());
+    if (!out || n < g.local_pixels) return fail(PT_E_INVALID, "output too small");
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels);
+    hipLaunchKernelGGL(k_camera, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    release_graph();
+    RC(download_paths(0, g.local_pixels, out));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_isect* isects) {
+    RC(need_init());
+    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range (capacity %d)", g.capacity);
+    if (n == 0) return PT_OK;
+    RC(upload_paths(0, paths, n));
+    RC(set_count(0, (int)n));
+    HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+    if (g.has_bvh)
+        hipLaunchKernelGGL((k_intersect<true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
+                           pathbuf(0), hits, staged_count(0));
+    else
+        hipLaunchKernelGGL((k_intersect<false>), dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0),
+                           hits, staged_count(0));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    std::vector<float4> nt(n);
+    std::vector<int> mat(n);
+    HIPCHK(hipMemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+        memset(&isects[i], 0, sizeof(pt_shadeable_isect));
+        isects[i].t = nt[i].w;
+        isects[i].surfaceNormal = pt_vec3{nt[i].x, nt[i].y, nt[i].z};
+        isects[i].materialId = mat[i];
+    }
+    release_graph();
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_path_segment* paths, int64_t n) {
+    RC(need_init());
+    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    if (n == 0) return PT_OK;
+    RC(upload_paths(0, paths, n));
+    RC(set_count(0, (int)n));
+    std::vector<float4> nt(n);
+    std::vector<int> mat(n);
+    for (int64_t i = 0; i < n; ++i) {
+        nt[i] = make_float4(isects[i].surfaceNormal.x, isects[i].surfaceNormal.y, isects[i].surfaceNormal.z,
+                            isects[i].t);
+        mat[i] = isects[i].materialId;
+        if (isects[i].t > 0.0f && (mat[i] < 0 || mat[i] >= std::max(1, g.sc.num_mats)))
+            return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
+    }
+    HIPCHK(hipMemcpy(g.d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+    hipLaunchKernelGGL(k_shade, dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), hits,
+                       (const int*)nullptr, staged_count(0), (const FrameCtl*)g.d_ctl, iteration, (float*)nullptr,
+                       (int*)nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    release_graph();
+    RC(download_paths(0, n, paths));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment* out, int64_t* alive_out) {
+    RC(need_init());
+    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    RC(upload_paths(0, paths, n));
+    std::vector<int> al(std::max<int64_t>(1, n));
+    for (int64_t i = 0; i < n; ++i) al[i] = paths[i].remainingBounces > 0;   // PathAlive
+    if (n) HIPCHK(hipMemcpy(g.d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    RC(set_count(0, (int)n));
+    const int ntiles = (int)((n + CTILE - 1) / CTILE);
+    HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * (size_t)(ntiles + 1)));
+    if (ntiles > 0) {
+        hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(0), pathbuf(1),
+                           (const int*)g.d_alive, staged_count(0), &g.d_ctl->cnt[1][0], &g.d_ctl->ticket[0],
+                           g.d_status, 7u);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(g.stream));
+    int na = 0;
+    HIPCHK(hipMemcpy(&na, &g.d_ctl->cnt[1][0], sizeof(int), hipMemcpyDeviceToHost));
+    if (alive_out) *alive_out = na;
+    release_graph();
+    RC(download_paths(1, na, out));
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm) {
+    RC(need_init());
+    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    if (n == 0) return PT_OK;
+    const int nk = std::max(1, g.sc.num_mats);
+    std::vector<int> mat(n);
+    for (int64_t i = 0; i < n; ++i) {
+        mat[i] = isects[i].materialId;
+        if (mat[i] < 0 || mat[i] >= nk) return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
+    }
+    HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    RC(set_count(0, (int)n));
+    const int ntiles = (int)((n + CTILE - 1) / CTILE);
+    hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
+                       g.d_tile_hist);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, staged_count(0), nk);
+    hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
+                       g.key_bits, g.d_tile_hist, g.d_perm);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemcpy(perm, g.d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
+    release_graph();
+    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    return PT_OK;
+}
+
+int32_t pt_test_rng(const int32_t* iid, int64_t m, int32_t n, float* out) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
+    if (m <= 0 || n <= 0) return PT_OK;
+    int* d_iid = nullptr;
+    float* d_out = nullptr;
+    HIPCHK(hipMalloc(&d_iid, sizeof(int) * 3 * m));
+    HIPCHK(hipMalloc(&d_out, sizeof(float) * m * n));
+    HIPCHK(hipMemcpy(d_iid, iid, sizeof(int) * 3 * m, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_rng, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, 0, d_iid, (int)m, n, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(out, d_out, sizeof(float) * m * n, hipMemcpyDeviceToHost));
+    (void)hipFree(d_iid);
+    (void)hipFree(d_out);
+    return PT_OK;
+}
+
+int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4* pbo) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
+    if (n <= 0) return PT_OK;
+    float* d_img = nullptr;
+    pt_uchar4* d_pbo = nullptr;
+    HIPCHK(hipMalloc(&d_img, sizeof(float) * 3 * n));
+    HIPCHK(hipMalloc(&d_pbo, sizeof(pt_uchar4) * n));
+    HIPCHK(hipMemcpy(d_img, image, sizeof(float) * 3 * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_to_pbo, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0, d_img, d_pbo, (int)n,
+                       iteration);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(pbo, d_pbo, sizeof(pt_uchar4) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(d_img);
+    (void)hipFree(d_pbo);
+    return PT_OK;
+}
+
+int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_times* out) {
+    RC(need_init());
+    if (!out || count <= 0) return fail(PT_E_INVALID, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    // eager launches, a HIP event after every kernel, no host synchronisation until the end
+    std::vector<hipEvent_t> ev;
+    std::vector<int> kind;
+    std::vector<size_t> frame_start;
+    for (int f = 0; f < count; ++f) {
+        hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, first_iteration + f,
+                           g.local_pixels);
+        if (g.opts.pipeline == PT_PIPELINE_STAGED && g.opts.stream_compaction)
+            HIPCHK(hipMemsetAsync(g.d_status, 0, sizeof(uint64_t) * (size_t)((g.capacity + CTILE - 1) / CTILE + 1),
+                                  g.stream));
+        frame_start.push_back(ev.size());
+        RC(enqueue_frame_body(&ev, &kind));
+        g.frames_done++;
+        g.last_iter = first_iteration + f;
+    }
+    HIPCHK(hipStreamSynchronize(g.stream));
+    double bounce_ms[MAXB] = {0};
+    double frame_ms = 0, compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0;
+    for (int f = 0; f < count; ++f) {
+        size_t a = frame_start[f], b = (f + 1 < count) ? frame_start[f + 1] : ev.size();
+        float total = 0;
+        (void)hipEventElapsedTime(&total, ev[a], ev[b - 1]);
+        frame_ms += total;
+        int bi = 0;
+        for (size_t i = a + 1; i < b; ++i) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
+            int k = kind[i];
+            if (k >= 100) bounce_ms[k - 100] += ms;
+            else if (k == 0) cam_ms += ms;
+            else if (k == 1) isect_ms += ms;
+            else if (k == 2) shade_ms += ms;
+            else if (k == 3) { compact_ms += ms; if (bi < MAXB) bounce_ms[bi++] += ms; }
+            else if (k == 4) sort_ms += ms;
+        }
+    }
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    out->frames = count;
+    out->frame_ms = (float)(frame_ms / count);
+    for (int b = 0; b < MAXB; ++b) out->bounce_ms[b] = (float)(bounce_ms[b] / count);
+    out->compact_ms = (float)(compact_ms / count);
+    out->intersect_ms = (float)(isect_ms / count);
+    out->shade_ms = (float)(shade_ms / count);
+    out->camera_ms = (float)(cam_ms / count);
+    out->sort_ms = (float)(sort_ms / count);
+    return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// scene_abi.cpp — C-ABI access to the C++ scene loader (for the Python harness and any
+// non-C++ caller): load a reference JSON scene, get the flat pt_scene_view pt_init takes.
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "scene.h"
+
+struct pt_scene_file {
+    Scene* scene;
+};
+
+namespace {
+thread_local std::string g_scene_err;
+}
+
+extern "C" {
+
+const char* pt_scene_last_error(void) { return g_scene_err.c_str(); }
+
+// res <= 0 / depth < 0 keep the file's values; viewer_camera != 0 applies main.cpp's camera
+// recompute (what every reference frame actually renders with)
+int32_t pt_scene_load(const char* path, int32_t resx, int32_t resy, int32_t depth, int32_t viewer_camera,
+                      pt_scene_file** out) {
+    if (!path || !out) return PT_E_INVALID;
+    try {
+        Scene* s = new Scene(path, resx, resy, depth);
+        if (viewer_camera) applyViewerCamera(s->state.camera);
+        *out = new pt_scene_file{s};
+        return PT_OK;
+    } catch (const std::exception& e) {
+        g_scene_err = e.what();
+        return PT_E_INVALID;
+    }
+}
+
+int32_t pt_scene_get_view(const pt_scene_file* f, pt_scene_view* v) {
+    if (!f || !v) return PT_E_INVALID;
+    *v = f->scene->view();
+    return PT_OK;
+}
+
+int32_t pt_scene_get_info(const pt_scene_file* f, int32_t* iterations, int32_t* trace_depth, char* image_name,
+                          int32_t cap) {
+    if (!f) return PT_E_INVALID;
+    if (iterations) *iterations = (int32_t)f->scene->state.iterations;
+    if (trace_depth) *trace_depth = f->scene->state.traceDepth;
+    if (image_name && cap > 0) {
+        std::strncpy(image_name, f->scene->state.imageName.c_str(), (size_t)cap - 1);
+        image_name[cap - 1] = 0;
+    }
+    return PT_OK;
+}
+
+int32_t pt_scene_material_name(const pt_scene_file* f, int32_t id, char* buf, int32_t cap) {
+    if (!f || id < 0 || id >= (int32_t)f->scene->materialNames.size() || !buf || cap <= 0) return PT_E_INVALID;
+    std::strncpy(buf, f->scene->materialNames[id].c_str(), (size_t)cap - 1);
+    buf[cap - 1] = 0;
+    return PT_OK;
+}
+
+void pt_scene_free(pt_scene_file* f) {
+    if (!f) return;
+    delete f->scene;
+    delete f;
+}
+
+}  // extern "C"
