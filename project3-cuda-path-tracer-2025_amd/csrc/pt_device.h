@@ -89,16 +89,20 @@ PT_DEV f3 xform(const float* m, f3 v, float w) {
     return f3{r0, r1, r2};
 }
 
-// 160-byte geom: inverseTransform | transform | invTranspose (affine rows) + type + material
+// 192-byte geom: inverseTransform | transform | invTranspose (affine rows), a conservative
+// world-space box (center, half extents incl. a safety margin) used only to SKIP exact tests
+// that cannot change the result, + type + material
 struct DevGeom {
     float inv[12];
     float fwd[12];
     float itr[12];
+    float box_c[3];
+    float box_h[3];
     int32_t type;
     int32_t materialid;
-    int32_t _pad[2];
+    int32_t _pad[4];
 };
-static_assert(sizeof(DevGeom) == 160, "DevGeom");
+static_assert(sizeof(DevGeom) == 192, "DevGeom");
 
 // 48-byte material: only what shading reads (sceneStructs.h:36-57)
 struct DevMaterial {

@@ -164,13 +164,37 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
 // computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
 // decides the winner (t and the normal "seed"); the world normal is derived once for the
 // winner — the same value the reference computes for every candidate and then keeps.
+// Conservative pre-test of one geom (approximate arithmetic, never decides a result): true
+// when the exact test is CERTAIN not to update (t_min, winner) — the ray line misses the geom's
+// margin-expanded world box, or enters it farther than t_min.  NaN anywhere: never skips.
+PT_DEV bool cull_geom(const DevGeom& g, f3 ro, f3 invd, float rdlen, float t_min) {
+    float t0 = -1e-2f, t1 = FLT_MAX_;
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float o = comp(ro, k) - g.box_c[k];
+        float id = comp(invd, k);
+        float ta = (-g.box_h[k] - o) * id;
+        float tb = (g.box_h[k] - o) * id;
+        nan |= (ta != ta) | (tb != tb);
+        t0 = __builtin_fmaxf(t0, __builtin_fminf(ta, tb));
+        t1 = __builtin_fminf(t1, __builtin_fmaxf(ta, tb));
+    }
+    if (nan || rdlen != rdlen) return false;
+    if (t1 < t0) return true;                                       // certain miss
+    return t0 > 0.0f && t0 * rdlen * (1.0f - 1e-5f) - 1e-4f > t_min;  // certainly farther
+}
+
 template <bool HAS_BVH>
 PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
     float t_min = FLT_MAX_;
     int win = -1;
     f3 seed = mk(0.f, 0.f, 0.f);
+    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
     for (int i = 0; i < sc.num_geoms; ++i) {
         const DevGeom& g = sc.geoms[i];
+        if (cull_geom(g, ro, invd, rdlen, t_min)) continue;
         f3 s;
         float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
         if (t > 0.0f && t_min > t) {

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -799,6 +800,20 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             }
         d.type = gg.type;
         d.materialid = gg.materialid;
+        // world box of the transformed unit cube (contains the radius-0.5 sphere too), grown by
+        // a margin far above every rounding the exact test can make: 1e-3 of the largest half
+        // extent + 1e-3 absolute (object-space pull-back 1e-4 times the scale)
+        float hmax = 0.f;
+        for (int r = 0; r < 3; ++r) {
+            d.box_c[r] = d.fwd[9 + r];
+            d.box_h[r] = 0.5f * (std::fabs(d.fwd[r]) + std::fabs(d.fwd[3 + r]) + std::fabs(d.fwd[6 + r]));
+            hmax = std::max(hmax, d.box_h[r]);
+        }
+        for (int r = 0; r < 3; ++r) d.box_h[r] += 1e-3f * hmax + 1e-3f * std::max(1.0f, hmax);
+        bool finite = std::isfinite(hmax) && std::isfinite(d.box_c[0]) && std::isfinite(d.box_c[1]) &&
+                      std::isfinite(d.box_c[2]);
+        if (!finite)   // degenerate transform: a box that never culls
+            for (int r = 0; r < 3; ++r) { d.box_c[r] = 0.f; d.box_h[r] = 3.0e38f; }
     }
     std::vector<DevMaterial> mats(std::max(1, s->num_materials));
     for (int i = 0; i < s->num_materials; ++i) {

@@ -88,7 +88,7 @@ def _oracle_isects(oracle, a, paths):
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy", "cornell_obj_khaslana"])
 def test_intersect_bitexact(name, oracle, ptamd):
-    a, b = _oracle_pair(oracle, ptamd, name, (32, 32))
+    a, b = _oracle_pair(oracle, ptamd, name, (96, 96))      # wavefront capacity >= 9216 paths
     tr = ptamd.PathTracer(b)
     paths = _random_paths(3000, 11)
     cam = tr.test_camera(3)
@@ -105,7 +105,7 @@ def test_intersect_bitexact(name, oracle, ptamd):
                                   "cornell_reflective_test", "cornell_transmissive_test", "cornell_obj_bnnuy"])
 def test_shade_bitexact(name, oracle, ptamd):
     import ctypes
-    a, b = _oracle_pair(oracle, ptamd, name, (48, 48))
+    a, b = _oracle_pair(oracle, ptamd, name, (80, 80))      # wavefront capacity >= 6400 paths
     tr = ptamd.PathTracer(b)
     paths = np.concatenate([tr.test_camera(2), _random_paths(2000, 5).astype(oracle.PATH)])
     isects = _oracle_isects(oracle, a, paths)
