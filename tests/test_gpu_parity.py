@@ -91,7 +91,7 @@ def test_intersect_bitexact(name, oracle, ptamd):
     a, b = _oracle_pair(oracle, ptamd, name, (96, 96))      # wavefront capacity >= 9216 paths
     tr = ptamd.PathTracer(b)
     paths = _random_paths(3000, 11)
-    cam = tr.test_camera(3)
+    cam = tr.test_camera(3)[:4000]
     paths = np.concatenate([paths.astype(oracle.PATH), cam])
     gpu = tr.test_intersect(paths)
     ref = _oracle_isects(oracle, a, paths)
@@ -107,7 +107,7 @@ def test_shade_bitexact(name, oracle, ptamd):
     import ctypes
     a, b = _oracle_pair(oracle, ptamd, name, (80, 80))      # wavefront capacity >= 6400 paths
     tr = ptamd.PathTracer(b)
-    paths = np.concatenate([tr.test_camera(2), _random_paths(2000, 5).astype(oracle.PATH)])
+    paths = np.concatenate([tr.test_camera(2)[:3000], _random_paths(2000, 5).astype(oracle.PATH)])
     isects = _oracle_isects(oracle, a, paths)
     s = a.c_struct()
     o = oracle.options(**BIT)
@@ -257,3 +257,23 @@ def test_cpp_boundary_pt_render(tmp_path, oracle):
         r.trace(it)
     assert _eq(data, r.image)
     assert os.path.getsize(out + ".png") > 64 * 64 * 3
+
+
+def test_pixel_shards_sum_to_full_frame(oracle, ptamd):
+    """PIXELS sharding (ptamd/dist.py): 3 row-band shards traced separately sum, exactly, to the
+    unsharded frame — what the RCCL combine does across GPUs."""
+    _, b = _oracle_pair(oracle, ptamd, "cornell_glass_test", (64, 50))
+    tr = ptamd.PathTracer(b)
+    tr.trace_frames(1, 2)
+    full = tr.image()
+    tr.free()
+    acc = np.zeros_like(full)
+    live = 0
+    for r in range(3):
+        tr = ptamd.PathTracer(b, shard_mode=ptamd.SHARD_PIXELS, shard_rank=r, shard_count=3, shard_rows=8)
+        tr.trace_frames(1, 2)
+        acc += tr.image()
+        live += tr.stats()["pixels"]
+        tr.free()
+    assert live == 64 * 50
+    assert _eq(acc, full)
