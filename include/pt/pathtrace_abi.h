@@ -71,6 +71,9 @@ typedef struct pt_options {
     int32_t shard_count;
     int32_t shard_rows;          /* PIXELS mode: height of the interleaved row bands (default 8) */
     int32_t block_size;          /* threads per block of the per-path kernels (default 256) */
+    int32_t variant;             /* fused-kernel variant bits (1: per-wave compaction atomics,
+                                    2: per-lane candidate queue for the geom tests); results are
+                                    bit-identical for every value */
 } pt_options;
 
 typedef struct pt_frame_stats {

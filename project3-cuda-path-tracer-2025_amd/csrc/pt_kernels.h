@@ -16,6 +16,13 @@ constexpr int NSEG = 8;        // output segments of the fused compaction (one p
 constexpr int MAXB = 64;       // max trace depth supported by the frame control block
 constexpr int BLOCK = 256;     // threads per block of the per-path kernels
 constexpr int MAXSTACK = 64;   // reference BVH stack (intersections.cu:167)
+constexpr int CNT_PAD = 32;    // one 128-byte cache line per live counter (atomics on separate lines)
+
+// kernel variants (pt_options.variant bits), selectable at run time for in-process A/B
+enum : int {
+    VAR_WAVE_ATOMIC = 1,   // compaction: one atomic per wave, no block barrier
+    VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
+};
 
 struct CamDev {
     int resx, resy;
@@ -49,7 +56,7 @@ struct FrameCtl {
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     int ticket[MAXB];                       // dynamic tile ids of the staged compaction kernel
-    int cnt[MAXB + 1][NSEG];                // paths entering bounce b, per output segment
+    int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
 };
 
 // a wavefront of paths: three float4 streams
@@ -161,9 +168,6 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
     return hit ? t_hit : -1.f;
 }
 
-// computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
-// decides the winner (t and the normal "seed"); the world normal is derived once for the
-// winner — the same value the reference computes for every candidate and then keeps.
 // Conservative pre-test of one geom (approximate arithmetic, never decides a result): true
 // when the exact test is CERTAIN not to update (t_min, winner) — the ray line misses the geom's
 // margin-expanded world box, or enters it farther than t_min.  NaN anywhere: never skips.
@@ -185,24 +189,10 @@ PT_DEV bool cull_geom(const DevGeom& g, f3 ro, f3 invd, float rdlen, float t_min
     return t0 > 0.0f && t0 * rdlen * (1.0f - 1e-5f) - 1e-4f > t_min;  // certainly farther
 }
 
+// winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
+// miss / facing conventions of pathtrace.cu:397-446
 template <bool HAS_BVH>
-PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
-    float t_min = FLT_MAX_;
-    int win = -1;
-    f3 seed = mk(0.f, 0.f, 0.f);
-    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
-    for (int i = 0; i < sc.num_geoms; ++i) {
-        const DevGeom& g = sc.geoms[i];
-        if (cull_geom(g, ro, invd, rdlen, t_min)) continue;
-        f3 s;
-        float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
-        if (t > 0.0f && t_min > t) {
-            t_min = t;
-            win = i;
-            seed = s;
-        }
-    }
+PT_DEV Hit finish_hit(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_min, int win, f3 seed) {
     Hit h;
     h.tri = -1;
     h.u = 0.f;
@@ -257,6 +247,65 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
     h.n = normal;
     h.mat = mat;
     return h;
+}
+
+// computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
+// decides the winner (t and the normal "seed"); the world normal is derived once for the
+// winner — the same value the reference computes for every candidate and then keeps.
+template <bool HAS_BVH>
+PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
+    float t_min = FLT_MAX_;
+    int win = -1;
+    f3 seed = mk(0.f, 0.f, 0.f);
+    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+    for (int i = 0; i < sc.num_geoms; ++i) {
+        const DevGeom& g = sc.geoms[i];
+        if (cull_geom(g, ro, invd, rdlen, t_min)) continue;
+        f3 s;
+        float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
+        if (t > 0.0f && t_min > t) {
+            t_min = t;
+            win = i;
+            seed = s;
+        }
+    }
+    return finish_hit<HAS_BVH>(sc, ro, rd, stack, t_min, win, seed);
+}
+
+// computeIntersections with the exact per-geom tests driven by a per-lane candidate queue:
+// pass 1 runs the cheap cull for every geom (certain misses drop out), pass 2 lets every lane
+// pop ITS next candidate (increasing geom index, so the first-minimum tie rule is unchanged)
+// and re-checks the cull against its current t_min before the exact test.  The wave executes
+// max-over-lanes(candidates) exact tests instead of one per geom any lane needs.
+template <bool HAS_BVH>
+PT_DEV Hit intersect_scene_q(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
+    if (sc.num_geoms > 64) return intersect_scene<HAS_BVH>(sc, ro, rd, stack);
+    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+    uint64_t cand = 0;
+    for (int i = 0; i < sc.num_geoms; ++i)
+        if (!cull_geom(sc.geoms[i], ro, invd, rdlen, FLT_MAX_)) cand |= 1ull << i;
+    float t_min = FLT_MAX_;
+    int win = -1;
+    f3 seed = mk(0.f, 0.f, 0.f);
+    while (__any(cand != 0)) {
+        if (cand != 0) {
+            const int i = __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const DevGeom& g = sc.geoms[i];
+            if (!cull_geom(g, ro, invd, rdlen, t_min)) {
+                f3 s;
+                float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
+                if (t > 0.0f && t_min > t) {
+                    t_min = t;
+                    win = i;
+                    seed = s;
+                }
+            }
+        }
+    }
+    return finish_hit<HAS_BVH>(sc, ro, rd, stack, t_min, win, seed);
 }
 
 // kernShadeMaterialProper for one live path (pathtrace.cu:521-621).  Textures: a material

@@ -43,17 +43,17 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels) {
     if (ctl->frames > 0) {
         for (int b = t; b < MAXB + 1; b += blockDim.x) {
             unsigned long long s = 0;
-            for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k];
+            for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k][0];
             ctl->tot[b] += s;
         }
     }
     __syncthreads();
-    for (int i = t; i < (MAXB + 1) * NSEG; i += blockDim.x) (&ctl->cnt[0][0])[i] = 0;
+    for (int i = t; i < (MAXB + 1) * NSEG * CNT_PAD; i += blockDim.x) (&ctl->cnt[0][0][0])[i] = 0;
     for (int i = t; i < MAXB; i += blockDim.x) ctl->ticket[i] = 0;
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
-        ctl->cnt[0][0] = local_pixels;
+        ctl->cnt[0][0][0] = local_pixels;
         ctl->frames += 1;
     }
 }
@@ -76,7 +76,7 @@ PT_DEV void gather_into_image(float* image, const PathReg& p) {
 // --------------------------------------------------------------------------------------------
 // FUSED: camera (bounce 0) | load -> intersect -> shade -> gather dead -> compact survivors
 // --------------------------------------------------------------------------------------------
-template <bool FIRST, bool HAS_BVH>
+template <bool FIRST, bool HAS_BVH, int VAR>
 __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride) {
     extern __shared__ int s_stack[];   // HAS_BVH: stack_depth x BLOCK ints
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     } else {
         segoff[0] = 0;
 #pragma unroll
-        for (int s = 0; s < NSEG; ++s) segoff[s + 1] = segoff[s] + ctl->cnt[bounce][s];
+        for (int s = 0; s < NSEG; ++s) segoff[s + 1] = segoff[s] + ctl->cnt[bounce][s][0];
         n = segoff[NSEG];
     }
     const int block_start = blockIdx.x * BLOCK;
@@ -110,16 +110,27 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             p = load_path(in, s * seg_stride + (gid - segoff[s]));
         }
         if (p.rb > 0) {
-            Hit h = intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
+            Hit h = (VAR & VAR_CAND_QUEUE) ? intersect_scene_q<HAS_BVH>(sc, p.o, p.d, s_stack + tid)
+                                           : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
             shade_path(sc, p, h, iter);
         }
     }
     const bool surv = active && p.rb > 0;
     if (active && !surv) gather_into_image(image, p);
 
-    // block-aggregated compaction: ballot -> per-wave counts -> one atomic per block
     const uint64_t m = __ballot(surv);
     const int lane = tid & 63, w = tid >> 6;
+    const int seg = blockIdx.x & (NSEG - 1);
+    if (VAR & VAR_WAVE_ATOMIC) {
+        // one returning atomic per wave on a counter that owns its cache line; no barrier
+        if (m == 0) return;
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&ctl->cnt[bounce + 1][seg][0], __popcll(m));
+        base = __shfl(base, 0);
+        if (surv) store_path(out, seg * seg_stride + base + mbcnt(m), p);
+        return;
+    }
+    // block-aggregated compaction: ballot -> per-wave counts -> one atomic per block
     if (lane == 0) s_wave[w] = __popcll(m);
     __syncthreads();
     if (tid == 0) {
@@ -130,8 +141,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             s_wave[i] = tot;
             tot += c;
         }
-        const int seg = blockIdx.x & (NSEG - 1);
-        s_base = tot ? seg * seg_stride + atomicAdd(&ctl->cnt[bounce + 1][seg], tot) : 0;
+        s_base = tot ? seg * seg_stride + atomicAdd(&ctl->cnt[bounce + 1][seg][0], tot) : 0;
     }
     __syncthreads();
     if (surv) store_path(out, s_base + s_wave[w] + mbcnt(m), p);
@@ -461,7 +471,31 @@ void release_graph() {
 }
 
 // device-side counter of the input of bounce b in the staged pipeline
-const int* staged_count(int b) { return &g.d_ctl->cnt[b][0]; }
+const int* staged_count(int b) { return &g.d_ctl->cnt[b][0][0]; }
+
+template <bool FIRST, bool HAS_BVH, int VAR>
+void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
+    hipLaunchKernelGGL((k_bounce<FIRST, HAS_BVH, VAR>), grid, dim3(BLOCK), HAS_BVH ? g.bvh_lds : 0, g.stream, g.sc,
+                       in, out, g.d_ctl, g.d_image, b, g.seg_stride);
+}
+template <bool FIRST, bool HAS_BVH>
+void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
+    switch (var) {
+        case 0: launch_bounce_t<FIRST, HAS_BVH, 0>(grid, in, out, b); break;
+        case 1: launch_bounce_t<FIRST, HAS_BVH, 1>(grid, in, out, b); break;
+        case 2: launch_bounce_t<FIRST, HAS_BVH, 2>(grid, in, out, b); break;
+        default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
+    }
+}
+void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
+    if (first) {
+        if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
+        else launch_bounce_v<true, false>(var, grid, in, out, b);
+    } else {
+        if (bvh) launch_bounce_v<false, true>(var, grid, in, out, b);
+        else launch_bounce_v<false, false>(var, grid, in, out, b);
+    }
+}
 
 // Enqueue one frame's kernels (everything after k_frame_begin) on g.stream.  `ev` (optional):
 // events recorded before the first and after every kernel, for pt_profile_frames.
@@ -482,22 +516,7 @@ int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            size_t lds = g.has_bvh ? g.bvh_lds : 0;
-            if (b == 0) {
-                if (g.has_bvh)
-                    hipLaunchKernelGGL((k_bounce<true, true>), dim3(nb), dim3(BLOCK), lds, g.stream, g.sc, in, out,
-                                       g.d_ctl, g.d_image, b, g.seg_stride);
-                else
-                    hipLaunchKernelGGL((k_bounce<true, false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, in, out,
-                                       g.d_ctl, g.d_image, b, g.seg_stride);
-            } else {
-                if (g.has_bvh)
-                    hipLaunchKernelGGL((k_bounce<false, true>), dim3(nb), dim3(BLOCK), lds, g.stream, g.sc, in, out,
-                                       g.d_ctl, g.d_image, b, g.seg_stride);
-                else
-                    hipLaunchKernelGGL((k_bounce<false, false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, in, out,
-                                       g.d_ctl, g.d_image, b, g.seg_stride);
-            }
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 3, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
             mark(100 + b);
         }
@@ -541,7 +560,7 @@ int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
             uint32_t epoch = (uint32_t)((g.frames_done * 64 + b + 1) & 0xffffff);
             // epoch in a captured graph is frozen; replays reset the status words instead
             hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(cur), pathbuf(cur ^ 1),
-                               (const int*)g.d_alive, n_in, &g.d_ctl->cnt[b + 1][0], &g.d_ctl->ticket[b], g.d_status,
+                               (const int*)g.d_alive, n_in, &g.d_ctl->cnt[b + 1][0][0], &g.d_ctl->ticket[b], g.d_status,
                                epoch);
             HIPCHK(hipGetLastError());
             mark(3);
@@ -695,7 +714,7 @@ int download_paths(int buf, int64_t n, pt_path_segment* out) {
     return PT_OK;
 }
 int set_count(int slot, int value) {
-    HIPCHK(hipMemcpy(&g.d_ctl->cnt[slot][0], &value, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(&g.d_ctl->cnt[slot][0][0], &value, sizeof(int), hipMemcpyHostToDevice));
     return PT_OK;
 }
 
@@ -731,6 +750,7 @@ void pt_default_options(pt_options* o) {
     o->shard_count = 1;
     o->shard_rows = 8;
     o->block_size = BLOCK;
+    o->variant = 0;
 }
 
 int32_t pt_init_data_container(int32_t* traced_depth) {
@@ -1023,7 +1043,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
         if (g.opts.pipeline == PT_PIPELINE_STAGED && !g.opts.stream_compaction) {
             s = b == 0 ? g.local_pixels : -1;   // no compaction: the live count is never formed
         } else {
-            for (int k = 0; k < NSEG; ++k) s += ctl.cnt[b][k];
+            for (int k = 0; k < NSEG; ++k) s += ctl.cnt[b][k][0];
         }
         out->live[b] = s;
         if (s > 0) out->segments += s;
@@ -1031,7 +1051,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
     out->frames_total = (int64_t)ctl.frames;
     for (int b = 0; b <= MAXB; ++b) {
         int64_t cur = 0;
-        for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k];
+        for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k][0];
         out->live_total[b] = (int64_t)ctl.tot[b] + (ctl.frames > 0 ? cur : 0);
         if (b < out->bounces) out->segments_total += out->live_total[b];
     }
@@ -1134,13 +1154,13 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * (size_t)(ntiles + 1)));
     if (ntiles > 0) {
         hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(0), pathbuf(1),
-                           (const int*)g.d_alive, staged_count(0), &g.d_ctl->cnt[1][0], &g.d_ctl->ticket[0],
+                           (const int*)g.d_alive, staged_count(0), &g.d_ctl->cnt[1][0][0], &g.d_ctl->ticket[0],
                            g.d_status, 7u);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(g.stream));
     int na = 0;
-    HIPCHK(hipMemcpy(&na, &g.d_ctl->cnt[1][0], sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&na, &g.d_ctl->cnt[1][0][0], sizeof(int), hipMemcpyDeviceToHost));
     if (alive_out) *alive_out = na;
     release_graph();
     RC(download_paths(1, na, out));

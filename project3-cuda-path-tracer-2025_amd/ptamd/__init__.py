@@ -56,7 +56,7 @@ class PtError(RuntimeError):
 class _Options(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "stream_compaction", "material_sort", "bvh", "arg_order", "pipeline", "use_graph", "device",
-        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size")]
+        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size", "variant")]
 
 
 class _SceneView(ctypes.Structure):
