@@ -750,7 +750,7 @@ void pt_default_options(pt_options* o) {
     o->shard_count = 1;
     o->shard_rows = 8;
     o->block_size = BLOCK;
-    o->variant = 0;
+    o->variant = VAR_CAND_QUEUE;   // fastest in the in-process A/B (tools/ab_variants.py)
 }
 
 int32_t pt_init_data_container(int32_t* traced_depth) {

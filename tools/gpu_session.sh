@@ -22,9 +22,12 @@ if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 100 --warmup 10
+    step bench_staged 600 python bench.py --steps 100 --warmup 10 --pipeline staged --no-cpu-baseline
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
         python bench.py --steps 30 --warmup 3 --no-cpu-baseline
+    step rocprof_staged 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_staged" -o run --output-format csv -- \
+        python bench.py --steps 30 --warmup 3 --no-cpu-baseline --pipeline staged
 fi
 echo "session done"
