@@ -202,17 +202,24 @@ __global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBu
 }
 
 // ---- stable compaction: tile-local ballot scan + decoupled look-back ----
-constexpr int CITEMS = 8;                       // items per thread
-constexpr int CTILE = BLOCK * CITEMS;           // 2048 items per tile
+// Tile = BLOCK x CITEMS items in item order k-major then lane.  Flags are counted first, the
+// tile's survivors are LOADED into registers (all loads in flight at once), and only then does
+// one lane walk the look-back chain — so the chain's hop latency overlaps the payload loads;
+// the stores follow.  Order of survivors == input order (thrust::stable_partition semantics).
+constexpr int CITEMS = 4;                       // items per thread
+constexpr int CTILE = BLOCK * CITEMS;           // 1024 items per tile
+constexpr int STILE = BLOCK * 8;                // material-sort tile (2048 items)
 constexpr uint64_t ST_AGG = 1ull << 32, ST_INC = 2ull << 32;
 
 PT_DEV uint64_t st_load(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 PT_DEV void st_store(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // status word: [63:40] epoch  [39:32] flag (1 aggregate, 2 inclusive)  [31:0] count
-__global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, const int* __restrict__ alive,
-                                                   const int* n_ptr, int* n_out, int* ticket,
-                                                   uint64_t* status, uint32_t epoch) {
+__global__ __launch_bounds__(BLOCK) void k_compact(const float4* __restrict__ inA, const float4* __restrict__ inB,
+                                                   const float4* __restrict__ inC, float4* __restrict__ outA,
+                                                   float4* __restrict__ outB, float4* __restrict__ outC,
+                                                   const int* __restrict__ alive, const int* n_ptr, int* n_out,
+                                                   int* ticket, uint64_t* status, uint32_t epoch) {
     __shared__ int s_cnt[CITEMS][BLOCK / 64];
     __shared__ int s_tile;
     __shared__ int s_prefix;
@@ -225,22 +232,45 @@ __global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, cons
     if (base >= n) return;
     bool f[CITEMS];
     uint64_t m[CITEMS];
+    int av[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) av[k] = alive[base + k * BLOCK + tid];   // capacity is tile-padded
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) f[k] = (base + k * BLOCK + tid < n) & (av[k] != 0);
+    // payload loads for the survivors, issued before any waiting
+    float4 a[CITEMS], b[CITEMS], c[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
         int idx = base + k * BLOCK + tid;
-        f[k] = idx < n && alive[idx] != 0;
+        if (f[k]) {
+            a[k] = inA[idx];
+            b[k] = inB[idx];
+            c[k] = inC[idx];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) {
         m[k] = __ballot(f[k]);
         if (lane == 0) s_cnt[k][w] = __popcll(m[k]);
     }
+    // pin the payload in registers here (otherwise hipcc sinks the loads past the look-back and
+    // issues them one item at a time)
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) {
+        if (f[k]) {
+            asm volatile("" : "+v"(a[k].x), "+v"(a[k].y), "+v"(a[k].z), "+v"(a[k].w));
+            asm volatile("" : "+v"(b[k].x), "+v"(b[k].y), "+v"(b[k].z), "+v"(b[k].w));
+            asm volatile("" : "+v"(c[k].x), "+v"(c[k].y), "+v"(c[k].z), "+v"(c[k].w));
+        }
+    }
     __syncthreads();
-    // tile aggregate and per-(k, wave) exclusive offsets, in item order (k-major, then wave)
     if (tid == 0) {
         int run = 0;
         for (int k = 0; k < CITEMS; ++k)
             for (int i = 0; i < BLOCK / 64; ++i) {
-                int c = s_cnt[k][i];
+                int cc = s_cnt[k][i];
                 s_cnt[k][i] = run;
-                run += c;
+                run += cc;
             }
         const uint64_t tag = (uint64_t)epoch << 40;
         int excl = 0;
@@ -250,14 +280,14 @@ __global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, cons
             st_store(&status[tile], tag | ST_AGG | (uint32_t)run);
             uint32_t spins = 0;
             for (int t = tile - 1; t >= 0;) {
-                uint64_t s = st_load(&status[t]);
-                if ((s >> 40) != epoch || ((s >> 32) & 0xff) == 0) {
+                uint64_t st = st_load(&status[t]);
+                if ((st >> 40) != epoch || ((st >> 32) & 0xff) == 0) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1u << 22)) break;   // bounded: never hang the GPU (result then wrong, flagged by tests)
                     continue;                          // predecessor not published yet
                 }
-                excl += (int)(uint32_t)s;
-                if (((s >> 32) & 0xff) == 2) break;
+                excl += (int)(uint32_t)st;
+                if (((st >> 32) & 0xff) == 2) break;
                 --t;
             }
             st_store(&status[tile], tag | ST_INC | (uint32_t)(excl + run));
@@ -270,11 +300,10 @@ __global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, cons
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
         if (f[k]) {
-            int idx = base + k * BLOCK + tid;
             int dst = prefix + s_cnt[k][w] + mbcnt(m[k]);
-            out.A[dst] = in.A[idx];
-            out.B[dst] = in.B[idx];
-            out.C[dst] = in.C[idx];
+            outA[dst] = a[k];
+            outB[dst] = b[k];
+            outC[dst] = c[k];
         }
     }
 }
@@ -282,16 +311,16 @@ __global__ __launch_bounds__(BLOCK) void k_compact(PathBuf in, PathBuf out, cons
 // ---- stable counting sort of materialId (MATERIAL_SORTING, pathtrace.cu:730-735) ----
 constexpr int MAXMAT = 256;
 
-// per-tile key histogram, tile = CTILE items
+// per-tile key histogram, tile = STILE items
 __global__ __launch_bounds__(BLOCK) void k_sort_hist(const int* __restrict__ keys, const int* n_ptr, int nkeys,
                                                      int* tile_hist) {
     __shared__ int h[MAXMAT];
     const int n = *n_ptr;
-    const int tile = blockIdx.x, base = tile * CTILE;
+    const int tile = blockIdx.x, base = tile * STILE;
     for (int i = threadIdx.x; i < nkeys; i += BLOCK) h[i] = 0;
     __syncthreads();
     if (base < n) {
-        for (int k = 0; k < CITEMS; ++k) {
+        for (int k = 0; k < STILE / BLOCK; ++k) {
             int idx = base + k * BLOCK + threadIdx.x;
             if (idx < n) atomicAdd(&h[keys[idx]], 1);
         }
@@ -303,7 +332,7 @@ __global__ __launch_bounds__(BLOCK) void k_sort_hist(const int* __restrict__ key
 // exclusive scan over (key, tile) in key-major order; one block
 __global__ __launch_bounds__(BLOCK) void k_sort_scan(int* tile_hist, const int* n_ptr, int nkeys) {
     const int n = *n_ptr;
-    const int ntiles = (n + CTILE - 1) / CTILE;
+    const int ntiles = (n + STILE - 1) / STILE;
     __shared__ int key_tot[MAXMAT];
     __shared__ int key_off[MAXMAT];
     for (int key = threadIdx.x; key < nkeys; key += BLOCK) {
@@ -332,12 +361,12 @@ __global__ __launch_bounds__(BLOCK) void k_sort_scatter(const int* __restrict__ 
     __shared__ int run[MAXMAT];           // items of each key already placed in this tile
     __shared__ int wcnt[BLOCK / 64][MAXMAT];
     const int n = *n_ptr;
-    const int tile = blockIdx.x, base = tile * CTILE;
+    const int tile = blockIdx.x, base = tile * STILE;
     if (base >= n) return;
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < nkeys; i += BLOCK) run[i] = 0;
     __syncthreads();
-    for (int k = 0; k < CITEMS; ++k) {
+    for (int k = 0; k < STILE / BLOCK; ++k) {
         int idx = base + k * BLOCK + tid;
         bool valid = idx < n;
         int key = valid ? keys[idx] : 0;
@@ -526,7 +555,8 @@ int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
     hipLaunchKernelGGL(k_camera, dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
     HIPCHK(hipGetLastError());
     mark(0);
-    const int ntiles = (g.local_pixels + CTILE - 1) / CTILE;
+    const int ntiles = (g.local_pixels + CTILE - 1) / CTILE;   // compaction tiles
+    const int stiles = (g.local_pixels + STILE - 1) / STILE;   // material-sort tiles
     int cur = 0;
     for (int b = 0; b < nbounces; ++b) {
         // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
@@ -543,10 +573,10 @@ int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
         const int* perm = nullptr;
         if (g.opts.material_sort) {
             const int nk = std::max(1, g.sc.num_mats);
-            hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
+            hipLaunchKernelGGL(k_sort_hist, dim3(stiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
                                g.d_tile_hist);
             hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, n_in, nk);
-            hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
+            hipLaunchKernelGGL(k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
                                g.key_bits, g.d_tile_hist, g.d_perm);
             HIPCHK(hipGetLastError());
             perm = g.d_perm;
@@ -559,7 +589,8 @@ int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
         if (g.opts.stream_compaction) {
             uint32_t epoch = (uint32_t)((g.frames_done * 64 + b + 1) & 0xffffff);
             // epoch in a captured graph is frozen; replays reset the status words instead
-            hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(cur), pathbuf(cur ^ 1),
+            PathBuf pi = pathbuf(cur), po = pathbuf(cur ^ 1);
+            hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B, po.C,
                                (const int*)g.d_alive, n_in, &g.d_ctl->cnt[b + 1][0][0], &g.d_ctl->ticket[b], g.d_status,
                                epoch);
             HIPCHK(hipGetLastError());
@@ -804,7 +835,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     g.local_pixels = sh.local_pixels;
     const int nb = nblocks(std::max(1, g.local_pixels));
     g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK;
-    g.capacity = std::max(g.seg_stride * NSEG, ((g.local_pixels + CTILE - 1) / CTILE) * CTILE);
+    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels);
+    g.capacity = ((g.capacity + STILE - 1) / STILE) * STILE;   // tile-padded: kernels may read a whole tile
 
     // ---- scene -> device records ----
     std::vector<DevGeom> geoms(s->num_geoms);
@@ -1153,7 +1185,8 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     const int ntiles = (int)((n + CTILE - 1) / CTILE);
     HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * (size_t)(ntiles + 1)));
     if (ntiles > 0) {
-        hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pathbuf(0), pathbuf(1),
+        PathBuf pi = pathbuf(0), po = pathbuf(1);
+        hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B, po.C,
                            (const int*)g.d_alive, staged_count(0), &g.d_ctl->cnt[1][0][0], &g.d_ctl->ticket[0],
                            g.d_status, 7u);
         HIPCHK(hipGetLastError());
@@ -1180,7 +1213,7 @@ int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm)
     }
     HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
     RC(set_count(0, (int)n));
-    const int ntiles = (int)((n + CTILE - 1) / CTILE);
+    const int ntiles = (int)((n + STILE - 1) / STILE);
     hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
                        g.d_tile_hist);
     hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, staged_count(0), nk);
