@@ -7,7 +7,7 @@ A "step" is one pathtrace() frame: one sample for every pixel, all bounces, accu
 HBM-resident image (no host copy: pathtrace.cu's per-frame 7.68 MB D->H copy is outside `value`,
 its cost is reported separately as `pcie_ms_per_frame`).  With N > 1 (launched by
 torch.distributed.run, one rank per GPU) every rank traces full frames with its own iteration
-numbers (sample sharding, weak scaling: rank r traces iterations r+1, r+1+N, ...), and the
+numbers (sample sharding, weak scaling: rank r traces a contiguous block of iterations), and the
 accumulated framebuffers are summed to rank 0 with one RCCL reduce inside the timed region.
 
 Timing: W untimed frames, then barrier + device sync, K frames, device sync + barrier; the MAX over
@@ -32,7 +32,8 @@ SCENE = os.path.join(REPO, "scenes", "cornell.json")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
 REF_MS_PER_FRAME = 42.204      # reference README.md:136, RTX 3060 Laptop, compaction on
 STATE_BYTES = 48               # one path in flight: 3 x float4 (origin|pixel, dir|bounces, rgb|-)
-IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3
+IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3 (1-frame pass)
+PLANE_STORE_BYTES = 12         # terminated path of an F-frame pass: float3 store to its frame's plane
 
 
 def parse():
@@ -66,11 +67,12 @@ def main():
     tr = ptamd.PathTracer(scene, device=local, pipeline=pipeline)
     depth = scene.trace_depth
 
-    # warmup: iterations 1..W on rank 0's schedule (r + 1 + k*world)
-    it = rank + 1
-    for _ in range(args.warmup):
-        tr.trace_frames(it, 1)
-        it += world
+    # SAMPLES sharding: rank r traces the contiguous iteration block 1 + r*(W+K) .. (r+1)*(W+K)
+    # (ptamd.dist.sample_iterations), so its frames group into multi-frame passes
+    it = 1 + rank * (args.warmup + args.steps)
+    if args.warmup:
+        tr.trace_frames(it, args.warmup)
+        it += args.warmup
     tr.synchronize()
     tr.reset_stats()
 
@@ -85,10 +87,8 @@ def main():
     if world == 1:
         prof = tr.profile(it, args.steps)              # K frames, events after every kernel
     else:
-        # each rank: its own iterations, interleaved sample schedule
         prof = None
-        for k in range(args.steps):
-            tr.trace_frames(it + k * world, 1)
+        tr.trace_frames(it, args.steps)
         tr.synchronize()
         ptr, n = tr.image_device_ptr()
         img = _device_tensor(torch, ptr, n, local, tr)
@@ -128,12 +128,14 @@ def main():
             "data": "scenes/cornell.json from the reference (800x800, depth 8, 1 spp per step); no synthetic inputs",
             "config": {"workload": "cornell.json 800x800 depth 8, stream compaction on, sort off (BASELINE configs[1])",
                        "pipeline": args.pipeline, "segments_per_frame": round(segs / args.steps / world, 1),
+                       "frames_per_pass": st["frames_per_pass"],
                        "parallelism": f"sample-sharded x{world}" if world > 1 else "single GPU"},
         }
         if prof is not None:
             line["roofline"] = roofline(prof, st, args, depth)
-            line["kernels_ms_per_frame"] = {"frame": round(prof["frame_ms"], 4),
-                                            "bounce": [round(x, 4) for x in prof["bounce_ms"]]}
+            line["kernels"] = {"frame_ms": round(prof["frame_ms"], 4), "passes": prof["passes"],
+                               "per_launch_bounce_ms": [round(x, 4) for x in prof["bounce_ms"]],
+                               "combine_ms_per_frame": round(prof["combine_ms"], 4)}
         line["pcie_ms_per_frame"] = pcie_copy_ms(tr)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -155,31 +157,33 @@ def _device_tensor(torch, ptr, n, device, tr):
 
 
 def roofline(prof, st, args, depth):
-    """Dominant kernel = the fused bounce kernel (all `depth` launches of a frame, the same code):
-    algorithmic bytes per launch = 48 B per path read (bounce > 0) + 48 B per survivor written
-    + 24 B image read-modify-write per terminated path; / its average launch duration."""
+    """Dominant kernel, per launch.  Fused: the bounce kernel (camera|intersect|shade|gather|
+    compact; `depth` launches per pass of F frames): algorithmic bytes = 48 B per path read
+    (bounce > 0) + 48 B per survivor written + 24 B image read-modify-write (or 12 B plane store)
+    per terminated path.  Staged: the compaction scatter kernel: 4 B flag per path in + 96 B per
+    survivor (48 B read + 48 B written).  achieved = bytes per launch / average launch duration
+    (hipExtLaunchKernel dispatch timestamps, pt_profile_frames)."""
     tot = st["live_total"]                 # per-bounce live counts summed over the timed frames
-    k = st["frames_total"]
+    launches = depth * prof["passes"]
+    nbytes = 0
+    for b in range(depth):
+        n_in, n_out = tot[b], tot[b + 1] if b + 1 < len(tot) else 0
+        if args.pipeline == "fused":
+            gather = IMAGE_RMW_BYTES if st["frames_per_pass"] == 1 else PLANE_STORE_BYTES
+            nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + gather * (n_in - n_out)
+        else:
+            nbytes += 4 * n_in + 2 * STATE_BYTES * n_out
     if args.pipeline == "fused":
-        nbytes = 0
-        for b in range(depth):
-            n_in, n_out = tot[b], tot[b + 1] if b + 1 < len(tot) else 0
-            nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + IMAGE_RMW_BYTES * (n_in - n_out)
-        launches = depth
-        ms = sum(prof["bounce_ms"][:depth])
-        name = "k_bounce (fused camera|intersect|shade|gather|compact, 8 launches per frame)"
+        name = "k_bounce (fused camera|intersect|shade|gather|compact, one launch per bounce per pass)"
     else:
-        nbytes = sum(4 * tot[b] + 2 * STATE_BYTES * (tot[b + 1] if b + 1 < len(tot) else 0) for b in range(depth))
-        launches = depth
-        ms = prof["compact_ms"]
-        name = "k_compact (stable partition, decoupled look-back)"
-    bytes_per_launch = nbytes / (k * launches)
-    avg_ms = ms / launches
+        name = "k_compact_scatter (stable partition: flags + survivor payload move)"
+    bytes_per_launch = nbytes / launches
+    avg_ms = sum(prof["bounce_ms"][:depth]) / depth
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = _traffic(name)
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_ms, 5)}
+            "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_ms, 5), "launches": launches}
 
 
 def _traffic(name):
@@ -189,7 +193,7 @@ def _traffic(name):
         return None
     with open(p) as f:
         d = json.load(f)
-    key = "k_bounce" if name.startswith("k_bounce") else "k_compact"
+    key = "k_bounce" if name.startswith("k_bounce") else "k_compact_scatter"
     return d.get(key, {}).get("hbm_bytes_per_launch")
 
 

@@ -74,6 +74,10 @@ typedef struct pt_options {
     int32_t variant;             /* fused-kernel variant bits (1: per-wave compaction atomics,
                                     2: per-lane candidate queue for the geom tests); results are
                                     bit-identical for every value */
+    int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..16;
+                                    0 = auto: ~5.2M paths in flight).  The image is bit-identical
+                                    to frame-by-frame tracing: terminated paths of a pass land in
+                                    per-frame planes that are added in frame order. */
 } pt_options;
 
 typedef struct pt_frame_stats {
@@ -85,6 +89,8 @@ typedef struct pt_frame_stats {
     int64_t frames_total;        /* frames traced since pt_init / pt_reset_stats */
     int64_t live_total[65];      /* per-bounce live counts summed over those frames */
     int64_t segments_total;      /* path segments traced over those frames */
+    int32_t frames_per_pass;     /* resolved F; live[] / segments above cover the last pass */
+    int32_t last_pass_frames;
 } pt_frame_stats;
 
 int32_t pt_abi_version(void);
@@ -165,17 +171,22 @@ int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4*
 /* ---- kernel timing (HIP events on the library's stream) for bench.py ---- */
 typedef struct pt_kernel_times {
     int32_t frames;
-    float frame_ms;              /* average frame wall time between events */
-    float bounce_ms[64];         /* average per-bounce kernel time (fused) / per-stage sums (staged) */
+    float frame_ms;              /* stream time of the whole run / frames */
+    float bounce_ms[64];         /* per-launch kernel time of bounce b (see pt_profile_frames) */
     float compact_ms;            /* staged: total compaction-kernel time per frame */
     float intersect_ms, shade_ms, camera_ms, sort_ms;
-    int64_t compact_bytes;       /* algorithmic bytes moved by compaction per frame */
-    int64_t frame_bytes;         /* algorithmic bytes of the whole frame */
+    int64_t compact_bytes;       /* reserved */
+    int64_t frame_bytes;         /* reserved */
+    float compact_scan_ms;       /* staged: compaction count + scan kernels per frame (compact_ms = scatter) */
+    int32_t passes;              /* wavefront passes the `frames` frames were traced in */
+    float combine_ms;            /* k_combine (per-frame planes -> image) per frame */
 } pt_kernel_times;
-/* Trace `count` frames with iterations first_iteration.. eagerly, a HIP event recorded on the
- * library's stream after every kernel and no host synchronisation until all frames are queued;
- * returns per-kernel average durations.  bounce_ms[b]: fused bounce kernel b, or (staged) the
- * compaction kernel of bounce b. */
+/* Trace `count` frames with iterations first_iteration.. eagerly, every kernel launched with
+ * hipExtLaunchKernel start/stop events (timestamps of that dispatch itself) and no host
+ * synchronisation until all frames are queued; returns per-kernel average durations and the
+ * stream-level frame time.  bounce_ms[b]: average duration of ONE launch of the fused bounce
+ * kernel b, or (staged) of the compaction scatter kernel of bounce b; the other *_ms fields are
+ * per frame.  Frames are grouped into passes exactly as pt_trace_frames groups them. */
 int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_times* out);
 
 #ifdef __cplusplus

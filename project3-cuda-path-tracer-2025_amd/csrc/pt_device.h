@@ -477,6 +477,7 @@ struct PathReg {
     f3 o, d, c;
     int pix;
     int rb;
+    int slot;       // frame of the pass this path belongs to (iteration = pass iteration + slot)
 };
 
 PT_DEV void scatter(PathReg& p, f3 intersect, f3 normal, const DevMaterial& m, f3 mcolor, Rng& rng, int arg_order) {

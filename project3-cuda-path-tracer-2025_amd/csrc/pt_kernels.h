@@ -47,12 +47,14 @@ struct SceneDev {
     int trace_depth, arg_order, use_bvh, stack_depth;
     CamDev cam;
     ShardDev shard;
+    float* contrib;     // passes of F > 1 frames: [slot][pixel] float3 of each terminated path
 };
 
 // frame control block (device memory); zeroed / advanced by k_frame_begin every frame
 struct FrameCtl {
-    int iter;
-    int _pad[3];
+    int iter;           // iteration of the pass's first frame (slot s traces iter + s)
+    int batch;          // frames in the current pass
+    int _pad[2];
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     int ticket[MAXB];                       // dynamic tile ids of the staged compaction kernel
@@ -74,12 +76,13 @@ PT_DEV PathReg load_path(const PathBuf& b, int i) {
     p.d = mk(d.x, d.y, d.z);
     p.rb = __float_as_int(d.w);
     p.c = mk(c.x, c.y, c.z);
+    p.slot = __float_as_int(c.w);
     return p;
 }
 PT_DEV void store_path(const PathBuf& b, int i, const PathReg& p) {
     b.A[i] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
     b.B[i] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
-    b.C[i] = make_float4(p.c.x, p.c.y, p.c.z, 0.0f);
+    b.C[i] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot));
 }
 
 // local path id of this process -> global pixel index (PIXELS shard: interleaved row bands)
@@ -115,6 +118,7 @@ PT_DEV PathReg camera_ray(const CamDev& cam, int iter, int trace_depth, int inde
     p.d = normalize(focalPoint - p.o);
     p.pix = index;
     p.rb = trace_depth;
+    p.slot = 0;
     return p;
 }
 

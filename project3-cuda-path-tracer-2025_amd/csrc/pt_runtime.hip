@@ -18,6 +18,7 @@
 // A frame is captured once into a hipGraph and replayed; the iteration number lives in
 // device memory (k_frame_begin advances it), so the replay needs no parameter updates.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -36,9 +37,9 @@ using namespace ptd;
 // kernels
 // =============================================================================================
 
-// Fold the previous frame's live counts into the running totals, advance (or set) the
-// iteration and zero the per-frame counters.  One block.
-__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels) {
+// Fold the previous pass's live counts into the running totals, advance (or set) the
+// iteration, zero the per-pass counters and start a pass of `batch` frames.  One block.
+__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int batch) {
     int t = threadIdx.x;
     if (ctl->frames > 0) {
         for (int b = t; b < MAXB + 1; b += blockDim.x) {
@@ -53,8 +54,9 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels) {
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
-        ctl->cnt[0][0][0] = local_pixels;
-        ctl->frames += 1;
+        ctl->batch = batch;
+        ctl->cnt[0][0][0] = local_pixels * batch;
+        ctl->frames += batch;
     }
 }
 
@@ -66,11 +68,43 @@ PT_DEV int mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-PT_DEV void gather_into_image(float* image, const PathReg& p) {
+// A pixel receives one contribution per frame (finalGather, pathtrace.cu:217-227, adds every
+// path's colour once).  Single-frame pass: add it now.  Pass of F > 1 frames: store it in the
+// frame's contribution plane; k_combine adds the planes in frame order afterwards, so the
+// image sees the same float additions in the same order as F sequential frames.
+PT_DEV void gather_into_image(float* image, const SceneDev& sc, int batch, const PathReg& p) {
+    if (batch > 1) {
+        float* px = sc.contrib + 3 * ((size_t)p.slot * (size_t)(sc.cam.resx * sc.cam.resy) + (size_t)p.pix);
+        px[0] = p.c.x;
+        px[1] = p.c.y;
+        px[2] = p.c.z;
+        return;
+    }
     float* px = image + 3 * (size_t)p.pix;
     px[0] += p.c.x;
     px[1] += p.c.y;
     px[2] += p.c.z;
+}
+
+// end of a pass of F > 1 frames: image += plane 0, += plane 1, ... (local pixels only)
+__global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* ctl, float* __restrict__ image) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= sc.shard.local_pixels) return;
+    const int batch = ctl->batch;
+    if (batch <= 1) return;
+    const size_t pix = (size_t)shard_pixel(sc, l);
+    const size_t plane = (size_t)sc.cam.resx * sc.cam.resy;
+    float* px = image + 3 * pix;
+    float r = px[0], gch = px[1], b = px[2];
+    const float* c = sc.contrib + 3 * pix;
+    for (int k = 0; k < batch; ++k, c += 3 * plane) {
+        r += c[0];
+        gch += c[1];
+        b += c[2];
+    }
+    px[0] = r;
+    px[1] = gch;
+    px[2] = b;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -83,10 +117,11 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     __shared__ int s_wave[BLOCK / 64];
     __shared__ int s_base;
     const int iter = ctl->iter;
+    const int batch = ctl->batch;
     int n;
     int segoff[NSEG + 1];
     if (FIRST) {
-        n = sc.shard.local_pixels;
+        n = ctl->cnt[0][0][0];          // local_pixels x batch
     } else {
         segoff[0] = 0;
 #pragma unroll
@@ -102,7 +137,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     p.rb = 0;
     if (active) {
         if (FIRST) {
-            p = camera_ray(sc.cam, iter, sc.trace_depth, shard_pixel(sc, gid));
+            const int slot = gid / sc.shard.local_pixels;
+            p = camera_ray(sc.cam, iter + slot, sc.trace_depth, shard_pixel(sc, gid - slot * sc.shard.local_pixels));
+            p.slot = slot;
         } else {
             int s = 0;
 #pragma unroll
@@ -112,11 +149,11 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         if (p.rb > 0) {
             Hit h = (VAR & VAR_CAND_QUEUE) ? intersect_scene_q<HAS_BVH>(sc, p.o, p.d, s_stack + tid)
                                            : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
-            shade_path(sc, p, h, iter);
+            shade_path(sc, p, h, iter + p.slot);
         }
     }
     const bool surv = active && p.rb > 0;
-    if (active && !surv) gather_into_image(image, p);
+    if (active && !surv) gather_into_image(image, sc, batch, p);
 
     const uint64_t m = __ballot(surv);
     const int lane = tid & 63, w = tid >> 6;
@@ -157,8 +194,11 @@ struct HitBuf {
 
 __global__ __launch_bounds__(BLOCK) void k_camera(SceneDev sc, PathBuf out, FrameCtl* ctl) {
     int gid = blockIdx.x * BLOCK + threadIdx.x;
-    if (gid >= sc.shard.local_pixels) return;
-    store_path(out, gid, camera_ray(sc.cam, ctl->iter, sc.trace_depth, shard_pixel(sc, gid)));
+    if (gid >= ctl->cnt[0][0][0]) return;
+    const int slot = gid / sc.shard.local_pixels;
+    PathReg p = camera_ray(sc.cam, ctl->iter + slot, sc.trace_depth, shard_pixel(sc, gid - slot * sc.shard.local_pixels));
+    p.slot = slot;
+    store_path(out, gid, p);
 }
 
 template <bool HAS_BVH>
@@ -195,49 +235,90 @@ __global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBu
     h.tri = -1;
     h.u = h.v = 0.f;
     const int iter = iter_override > 0 ? iter_override : ctl->iter;
-    shade_path(sc, p, h, iter);
+    shade_path(sc, p, h, iter + p.slot);
     store_path(buf, i, p);
-    if (p.rb <= 0 && image) gather_into_image(image, p);
+    if (p.rb <= 0 && image) gather_into_image(image, sc, iter_override > 0 ? 1 : ctl->batch, p);
     if (alive) alive[i] = p.rb > 0;
 }
 
-// ---- stable compaction: tile-local ballot scan + decoupled look-back ----
-// Tile = BLOCK x CITEMS items in item order k-major then lane.  Flags are counted first, the
-// tile's survivors are LOADED into registers (all loads in flight at once), and only then does
-// one lane walk the look-back chain — so the chain's hop latency overlaps the payload loads;
-// the stores follow.  Order of survivors == input order (thrust::stable_partition semantics).
+// ---- stable compaction (thrust::stable_partition(PathAlive), pathtrace.cu:750-757) ----
+// Reduce-then-scan, three launches with no inter-workgroup waiting (dispatch order on MI355X is
+// undefined by contract, and a single-word ticket / hop-by-hop look-back serialises at the
+// device-scope atomic rate):
+//   k_compact_count   per tile of CTILE items: popcount of ballot(alive) -> tile_cnt[t]
+//   k_compact_scan    one workgroup: exclusive scan of tile_cnt -> tile_off, total -> n_out
+//   k_compact_scatter per tile: flags + survivor payload loaded together, wave ballot/mbcnt
+//                     ranks in item order, stores to tile_off[t] + rank (stable)
 constexpr int CITEMS = 4;                       // items per thread
 constexpr int CTILE = BLOCK * CITEMS;           // 1024 items per tile
 constexpr int STILE = BLOCK * 8;                // material-sort tile (2048 items)
-constexpr uint64_t ST_AGG = 1ull << 32, ST_INC = 2ull << 32;
+constexpr int SCAN_THREADS = 1024;
 
-PT_DEV uint64_t st_load(const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-PT_DEV void st_store(uint64_t* p, uint64_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// status word: [63:40] epoch  [39:32] flag (1 aggregate, 2 inclusive)  [31:0] count
-__global__ __launch_bounds__(BLOCK) void k_compact(const float4* __restrict__ inA, const float4* __restrict__ inB,
-                                                   const float4* __restrict__ inC, float4* __restrict__ outA,
-                                                   float4* __restrict__ outB, float4* __restrict__ outC,
-                                                   const int* __restrict__ alive, const int* n_ptr, int* n_out,
-                                                   int* ticket, uint64_t* status, uint32_t epoch) {
-    __shared__ int s_cnt[CITEMS][BLOCK / 64];
-    __shared__ int s_tile;
-    __shared__ int s_prefix;
+__global__ __launch_bounds__(BLOCK) void k_compact_count(const int* __restrict__ alive, const int* n_ptr,
+                                                         int* __restrict__ tile_cnt) {
+    __shared__ int s_w[BLOCK / 64];
     const int n = *n_ptr;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1);
-    __syncthreads();
-    const int tile = s_tile;
-    const int base = tile * CTILE;
+    const int base = blockIdx.x * CTILE;
     if (base >= n) return;
-    bool f[CITEMS];
-    uint64_t m[CITEMS];
+    const int tid = threadIdx.x;
     int av[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) av[k] = alive[base + k * BLOCK + tid];   // capacity is tile-padded
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) c += __popcll(__ballot((base + k * BLOCK + tid < n) & (av[k] != 0)));
+    if ((tid & 63) == 0) s_w[tid >> 6] = c;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) t += s_w[i];
+        tile_cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_compact_scan(const int* __restrict__ tile_cnt, const int* n_ptr,
+                                                                int* __restrict__ tile_off, int* n_out) {
+    __shared__ int s_part[SCAN_THREADS];
+    const int n = *n_ptr;
+    const int ntiles = (n + CTILE - 1) / CTILE;
+    const int per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
+    const int tid = threadIdx.x;
+    const int lo = tid * per, hi = min(ntiles, lo + per);
+    int sum = 0;
+    for (int t = lo; t < hi; ++t) sum += tile_cnt[t];
+    s_part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < SCAN_THREADS; off <<= 1) {   // Hillis-Steele inclusive scan in LDS
+        int v = tid >= off ? s_part[tid - off] : 0;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    int run = tid ? s_part[tid - 1] : 0;
+    for (int t = lo; t < hi; ++t) {
+        tile_off[t] = run;
+        run += tile_cnt[t];
+    }
+    if (tid == SCAN_THREADS - 1) *n_out = s_part[SCAN_THREADS - 1];
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compact_scatter(const float4* __restrict__ inA, const float4* __restrict__ inB,
+                                                           const float4* __restrict__ inC, float4* __restrict__ outA,
+                                                           float4* __restrict__ outB, float4* __restrict__ outC,
+                                                           const int* __restrict__ alive, const int* n_ptr,
+                                                           const int* __restrict__ tile_off) {
+    __shared__ int s_cnt[CITEMS][BLOCK / 64];
+    const int n = *n_ptr;
+    const int base = blockIdx.x * CTILE;
+    if (base >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int av[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) av[k] = alive[base + k * BLOCK + tid];
+    bool f[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) f[k] = (base + k * BLOCK + tid < n) & (av[k] != 0);
-    // payload loads for the survivors, issued before any waiting
     float4 a[CITEMS], b[CITEMS], c[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
@@ -248,59 +329,28 @@ __global__ __launch_bounds__(BLOCK) void k_compact(const float4* __restrict__ in
             c[k] = inC[idx];
         }
     }
+    uint64_t m[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
         m[k] = __ballot(f[k]);
         if (lane == 0) s_cnt[k][w] = __popcll(m[k]);
     }
-    // pin the payload in registers here (otherwise hipcc sinks the loads past the look-back and
-    // issues them one item at a time)
+    __syncthreads();
+    // exclusive offsets in item order (k-major, then wave): every thread recomputes its own
+    int off[CITEMS];
+    int run = tile_off[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < CITEMS; ++k) {
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) {
+            if (i == w) off[k] = run;
+            run += s_cnt[k][i];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
         if (f[k]) {
-            asm volatile("" : "+v"(a[k].x), "+v"(a[k].y), "+v"(a[k].z), "+v"(a[k].w));
-            asm volatile("" : "+v"(b[k].x), "+v"(b[k].y), "+v"(b[k].z), "+v"(b[k].w));
-            asm volatile("" : "+v"(c[k].x), "+v"(c[k].y), "+v"(c[k].z), "+v"(c[k].w));
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int run = 0;
-        for (int k = 0; k < CITEMS; ++k)
-            for (int i = 0; i < BLOCK / 64; ++i) {
-                int cc = s_cnt[k][i];
-                s_cnt[k][i] = run;
-                run += cc;
-            }
-        const uint64_t tag = (uint64_t)epoch << 40;
-        int excl = 0;
-        if (tile == 0) {
-            st_store(&status[0], tag | ST_INC | (uint32_t)run);
-        } else {
-            st_store(&status[tile], tag | ST_AGG | (uint32_t)run);
-            uint32_t spins = 0;
-            for (int t = tile - 1; t >= 0;) {
-                uint64_t st = st_load(&status[t]);
-                if ((st >> 40) != epoch || ((st >> 32) & 0xff) == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) break;   // bounded: never hang the GPU (result then wrong, flagged by tests)
-                    continue;                          // predecessor not published yet
-                }
-                excl += (int)(uint32_t)st;
-                if (((st >> 32) & 0xff) == 2) break;
-                --t;
-            }
-            st_store(&status[tile], tag | ST_INC | (uint32_t)(excl + run));
-        }
-        s_prefix = excl;
-        if (base + CTILE >= n) *n_out = excl + run;   // the last tile publishes the count
-    }
-    __syncthreads();
-    const int prefix = s_prefix;
-#pragma unroll
-    for (int k = 0; k < CITEMS; ++k) {
-        if (f[k]) {
-            int dst = prefix + s_cnt[k][w] + mbcnt(m[k]);
+            int dst = off[k] + mbcnt(m[k]);
             outA[dst] = a[k];
             outB[dst] = b[k];
             outC[dst] = c[k];
@@ -438,6 +488,11 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+#define RC(x)                      \
+    do {                           \
+        int rc_ = (x);             \
+        if (rc_ != PT_OK) return rc_; \
+    } while (0)
 #define HIPCHK(expr)                                                                              \
     do {                                                                                          \
         hipError_t e_ = (expr);                                                                   \
@@ -452,6 +507,9 @@ int dalloc(T** p, size_t n) {
     HIPCHK(hipMalloc((void**)p, n * sizeof(T)));
     return PT_OK;
 }
+
+constexpr int MAXF = 16;                    // frames per pass, upper bound
+constexpr int64_t AUTO_BATCH_PATHS = 5200000;   // 800x800: F = 8 (A/B: F=1 0.214, 2 0.161, 4 0.137, 8 0.129, 16 0.129 ms/frame)
 
 struct State {
     bool inited = false;
@@ -476,12 +534,15 @@ struct State {
     int* d_alive = nullptr;
     int* d_perm = nullptr;
     int* d_tile_hist = nullptr;
-    uint64_t* d_status = nullptr;
+    int* d_tile_cnt = nullptr;
+    int* d_tile_off = nullptr;
     float* d_image = nullptr;
     FrameCtl* d_ctl = nullptr;
-    // graph
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
+    float* d_contrib = nullptr;      // passes of F > 1 frames: F planes of pixels_total float3
+    int batch = 1;                   // frames per pass (pt_options.frames_per_pass, resolved)
+    // one captured pass per pass size (1..MAXF frames)
+    hipGraph_t graph[MAXF + 1] = {};
+    hipGraphExec_t graph_exec[MAXF + 1] = {};
     int last_iter = 0;
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
@@ -490,13 +551,38 @@ struct State {
 State g;
 
 PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path[i][2]}; }
+
+// pt_profile_frames: every kernel of the frame is launched with hipExtLaunchKernel's start/stop
+// events, which take their timestamps from that dispatch packet itself -- the kernel's own
+// execution time, independent of how far ahead of the GPU the host is.
+struct ProfRec {
+    int kind;            // -1 frame begin, 0 camera, 1 intersect, 2 shade, 3 compact scatter,
+                         // 4 material sort, 5 compact count+scan, 100+b fused bounce b
+    hipEvent_t start, stop;
+};
+std::vector<ProfRec>* g_prof = nullptr;
+
+template <class K, class... A>
+void launch(int kind, K kernel, dim3 grid, dim3 block, uint32_t lds, A... args) {
+    if (g_prof) {
+        ProfRec r{kind, nullptr, nullptr};
+        (void)hipEventCreate(&r.start);
+        (void)hipEventCreate(&r.stop);
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, g.stream, r.start, r.stop, 0, args...);
+        g_prof->push_back(r);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, g.stream, args...);
+    }
+}
 int nblocks(int n) { return (n + BLOCK - 1) / BLOCK; }
 
 void release_graph() {
-    if (g.graph_exec) (void)hipGraphExecDestroy(g.graph_exec);
-    if (g.graph) (void)hipGraphDestroy(g.graph);
-    g.graph_exec = nullptr;
-    g.graph = nullptr;
+    for (int f = 0; f <= MAXF; ++f) {
+        if (g.graph_exec[f]) (void)hipGraphExecDestroy(g.graph_exec[f]);
+        if (g.graph[f]) (void)hipGraphDestroy(g.graph[f]);
+        g.graph_exec[f] = nullptr;
+        g.graph[f] = nullptr;
+    }
 }
 
 // device-side counter of the input of bounce b in the staged pipeline
@@ -504,8 +590,8 @@ const int* staged_count(int b) { return &g.d_ctl->cnt[b][0][0]; }
 
 template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
-    hipLaunchKernelGGL((k_bounce<FIRST, HAS_BVH, VAR>), grid, dim3(BLOCK), HAS_BVH ? g.bvh_lds : 0, g.stream, g.sc,
-                       in, out, g.d_ctl, g.d_image, b, g.seg_stride);
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), HAS_BVH ? g.bvh_lds : 0, g.sc, in, out,
+           g.d_ctl, g.d_image, b, g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -526,123 +612,104 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     }
 }
 
-// Enqueue one frame's kernels (everything after k_frame_begin) on g.stream.  `ev` (optional):
-// events recorded before the first and after every kernel, for pt_profile_frames.
-int enqueue_frame_body(std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
+// Enqueue one pass's kernels (everything after k_frame_begin) on g.stream: `batch` frames
+// traced together as one wavefront of local_pixels x batch paths.
+int enqueue_pass_body(int batch) {
     const int depth = g.sc.trace_depth;
-    const int nb = nblocks(g.local_pixels);
-    auto mark = [&](int kind) {
-        if (ev) {
-            hipEvent_t e;
-            (void)hipEventCreate(&e);
-            (void)hipEventRecord(e, g.stream);
-            ev->push_back(e);
-            ev_kind->push_back(kind);
-        }
-    };
-    mark(-1);
+    const int npaths = g.local_pixels * batch;
+    const int nb = nblocks(npaths);
     const int nbounces = std::max(1, depth);
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
             launch_bounce(b == 0, g.has_bvh, g.opts.variant & 3, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
-            mark(100 + b);
         }
         return PT_OK;
     }
+    // STAGED (k_combine after the pass is enqueued by enqueue_pass)
     // STAGED
-    hipLaunchKernelGGL(k_camera, dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
+    launch(0, k_camera, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(0), g.d_ctl);
     HIPCHK(hipGetLastError());
-    mark(0);
-    const int ntiles = (g.local_pixels + CTILE - 1) / CTILE;   // compaction tiles
-    const int stiles = (g.local_pixels + STILE - 1) / STILE;   // material-sort tiles
+    const int ntiles = (npaths + CTILE - 1) / CTILE;   // compaction tiles
+    const int stiles = (npaths + STILE - 1) / STILE;   // material-sort tiles
     int cur = 0;
     for (int b = 0; b < nbounces; ++b) {
         // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
         const int* n_in = g.opts.stream_compaction ? staged_count(b) : staged_count(0);
         HitBuf hits{g.d_hit_nt, g.d_hit_mat};
         if (g.has_bvh)
-            hipLaunchKernelGGL((k_intersect<true>), dim3(nb), dim3(BLOCK), g.bvh_lds, g.stream, g.sc, pathbuf(cur),
-                               hits, n_in);
+            launch(1, k_intersect<true>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
         else
-            hipLaunchKernelGGL((k_intersect<false>), dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(cur), hits,
-                               n_in);
+            launch(1, k_intersect<false>, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, n_in);
         HIPCHK(hipGetLastError());
-        mark(1);
         const int* perm = nullptr;
         if (g.opts.material_sort) {
             const int nk = std::max(1, g.sc.num_mats);
-            hipLaunchKernelGGL(k_sort_hist, dim3(stiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
-                               g.d_tile_hist);
-            hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, n_in, nk);
-            hipLaunchKernelGGL(k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, n_in, nk,
-                               g.key_bits, g.d_tile_hist, g.d_perm);
+            launch(4, k_sort_hist, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.d_tile_hist);
+            launch(4, k_sort_scan, dim3(1), dim3(BLOCK), 0, g.d_tile_hist, n_in, nk);
+            launch(4, k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.key_bits,
+                   (const int*)g.d_tile_hist, g.d_perm);
             HIPCHK(hipGetLastError());
             perm = g.d_perm;
-            mark(4);
         }
-        hipLaunchKernelGGL(k_shade, dim3(nb), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(cur), hits, perm, n_in,
-                           (const FrameCtl*)g.d_ctl, 0, g.d_image, g.opts.stream_compaction ? g.d_alive : nullptr);
+        launch(2, k_shade, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, perm, n_in, (const FrameCtl*)g.d_ctl,
+               0, g.d_image, g.opts.stream_compaction ? g.d_alive : (int*)nullptr);
         HIPCHK(hipGetLastError());
-        mark(2);
         if (g.opts.stream_compaction) {
-            uint32_t epoch = (uint32_t)((g.frames_done * 64 + b + 1) & 0xffffff);
-            // epoch in a captured graph is frozen; replays reset the status words instead
             PathBuf pi = pathbuf(cur), po = pathbuf(cur ^ 1);
-            hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B, po.C,
-                               (const int*)g.d_alive, n_in, &g.d_ctl->cnt[b + 1][0][0], &g.d_ctl->ticket[b], g.d_status,
-                               epoch);
+            int* n_out = &g.d_ctl->cnt[b + 1][0][0];
+            launch(5, k_compact_count, dim3(ntiles), dim3(BLOCK), 0, (const int*)g.d_alive, n_in, g.d_tile_cnt);
+            launch(5, k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, (const int*)g.d_tile_cnt, n_in, g.d_tile_off,
+                   n_out);
+            launch(3, k_compact_scatter, dim3(ntiles), dim3(BLOCK), 0, (const float4*)pi.A, (const float4*)pi.B,
+                   (const float4*)pi.C, po.A, po.B, po.C, (const int*)g.d_alive, n_in, (const int*)g.d_tile_off);
             HIPCHK(hipGetLastError());
-            mark(3);
             cur ^= 1;
         }
     }
     return PT_OK;
 }
 
-int enqueue_frame(int set_iter, std::vector<hipEvent_t>* ev, std::vector<int>* ev_kind) {
-    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, set_iter, g.local_pixels);
+int enqueue_pass(int set_iter, int batch) {
+    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, g.d_ctl, set_iter, g.local_pixels, batch);
     HIPCHK(hipGetLastError());
-    if (g.opts.pipeline == PT_PIPELINE_STAGED && g.opts.stream_compaction) {
-        // look-back status words must not carry a previous frame's INCLUSIVE flag of the same epoch
-        HIPCHK(hipMemsetAsync(g.d_status, 0, sizeof(uint64_t) * (size_t)((g.capacity + CTILE - 1) / CTILE + 1),
-                              g.stream));
+    RC(enqueue_pass_body(batch));
+    if (batch > 1) {
+        launch(6, k_combine, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.sc, (const FrameCtl*)g.d_ctl,
+               g.d_image);
+        HIPCHK(hipGetLastError());
     }
-    return enqueue_frame_body(ev, ev_kind);
+    return PT_OK;
 }
 
-int build_graph() {
-    release_graph();
+int build_graph(int batch) {
     HIPCHK(hipStreamBeginCapture(g.stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_frame(0, nullptr, nullptr);
+    int rc = enqueue_pass(0, batch);
     hipGraph_t gr = nullptr;
     hipError_t e = hipStreamEndCapture(g.stream, &gr);
     if (rc != PT_OK) return rc;
     HIPCHK(e);
-    g.graph = gr;
-    HIPCHK(hipGraphInstantiate(&g.graph_exec, g.graph, nullptr, nullptr, 0));
+    g.graph[batch] = gr;
+    HIPCHK(hipGraphInstantiate(&g.graph_exec[batch], gr, nullptr, nullptr, 0));
     return PT_OK;
 }
 
-// one frame with iteration `iter`
-int run_frame(int iter) {
+// one pass: frames iter .. iter + batch - 1
+int run_pass(int iter, int batch) {
     if (g.opts.use_graph) {
-        if (!g.graph_exec) {
-            int rc = build_graph();
-            if (rc != PT_OK) return rc;
-        }
+        if (!g.graph_exec[batch]) RC(build_graph(batch));
         // the graph's k_frame_begin increments: preset iter - 1 (stream-ordered)
         HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&g.d_ctl->iter, iter - 1, 1, g.stream));
-        HIPCHK(hipGraphLaunch(g.graph_exec, g.stream));
+        HIPCHK(hipGraphLaunch(g.graph_exec[batch], g.stream));
     } else {
-        int rc = enqueue_frame(iter, nullptr, nullptr);
-        if (rc != PT_OK) return rc;
+        RC(enqueue_pass(iter, batch));
     }
-    g.last_iter = iter;
-    g.frames_done++;
+    g.last_iter = iter + batch - 1;
+    g.frames_done += batch;
     return PT_OK;
 }
+int run_frame(int iter) { return run_pass(iter, 1); }
 
 // max DFS stack the reference traversal can reach on this tree (no culling)
 int bvh_max_stack(const pt_bvh_node* nodes, int n) {
@@ -668,7 +735,7 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 void free_all() {
     release_graph();
     void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_alive,
-                    g.d_perm, g.d_tile_hist, g.d_status, g.d_image, g.d_ctl};
+                    g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < 2; ++i)
@@ -749,12 +816,6 @@ int set_count(int slot, int value) {
     return PT_OK;
 }
 
-#define RC(x)                      \
-    do {                           \
-        int rc_ = (x);             \
-        if (rc_ != PT_OK) return rc_; \
-    } while (0)
-
 int need_init() { return g.inited ? PT_OK : fail(PT_E_STATE, "pt_init has not been called"); }
 
 }  // namespace
@@ -782,6 +843,7 @@ void pt_default_options(pt_options* o) {
     o->shard_rows = 8;
     o->block_size = BLOCK;
     o->variant = VAR_CAND_QUEUE;   // fastest in the in-process A/B (tools/ab_variants.py)
+    o->frames_per_pass = 0;        // auto
 }
 
 int32_t pt_init_data_container(int32_t* traced_depth) {
@@ -793,6 +855,14 @@ int32_t pt_free(void) {
     if (g.inited) free_all();
     g.inited = false;
     return PT_OK;
+}
+
+// frames per pass when pt_options.frames_per_pass == 0: enough paths in flight to fill the
+// chip in the late, mostly-terminated bounces (~5.2M paths at bounce 0), at most MAXF
+int auto_batch(int local_pixels) {
+    int f = 1;
+    while (f * 2 <= MAXF && (int64_t)local_pixels * f * 2 <= AUTO_BATCH_PATHS) f *= 2;
+    return f;
 }
 
 int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
@@ -833,9 +903,13 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         sh.local_pixels = g.pixels_total;
     }
     g.local_pixels = sh.local_pixels;
-    const int nb = nblocks(std::max(1, g.local_pixels));
+    if (o.frames_per_pass < 0 || o.frames_per_pass > MAXF)
+        return fail(PT_E_INVALID, "frames_per_pass must be 0 (auto) .. %d", MAXF);
+    g.batch = o.frames_per_pass > 0 ? o.frames_per_pass : auto_batch(g.local_pixels);
+    if ((int64_t)g.local_pixels * g.batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
+    const int nb = nblocks(std::max(1, g.local_pixels * g.batch));
     g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK;
-    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels);
+    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels * g.batch);
     g.capacity = ((g.capacity + STILE - 1) / STILE) * STILE;   // tile-padded: kernels may read a whole tile
 
     // ---- scene -> device records ----
@@ -963,9 +1037,10 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     RC(dalloc(&g.d_perm, (size_t)g.capacity));
     const int ntiles = (g.capacity + CTILE - 1) / CTILE + 1;
     RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, s->num_materials)));
-    RC(dalloc(&g.d_status, (size_t)ntiles));
-    HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * ntiles));
+    RC(dalloc(&g.d_tile_cnt, (size_t)ntiles));
+    RC(dalloc(&g.d_tile_off, (size_t)ntiles));
     RC(dalloc(&g.d_image, (size_t)g.pixels_total * 3));
+    if (g.batch > 1) RC(dalloc(&g.d_contrib, (size_t)g.pixels_total * 3 * g.batch));
     HIPCHK(hipMemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
     RC(dalloc(&g.d_ctl, 1));
     HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
@@ -988,6 +1063,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.stack_depth = g.stack_depth;
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
+    sc.contrib = g.d_contrib;
     g.inited = true;
     HIPCHK(hipDeviceSynchronize());
     return PT_OK;
@@ -1026,7 +1102,12 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
 int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     RC(need_init());
     if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
-    for (int i = 0; i < count; ++i) RC(run_frame(first_iteration + i));
+    // passes of g.batch frames (bit-identical to frame-by-frame: k_combine keeps the order)
+    for (int i = 0; i < count;) {
+        const int f = std::min(g.batch, count - i);
+        RC(run_pass(first_iteration + i, f));
+        i += f;
+    }
     return PT_OK;
 }
 
@@ -1073,7 +1154,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
     for (int b = 0; b < out->bounces; ++b) {
         int64_t s = 0;
         if (g.opts.pipeline == PT_PIPELINE_STAGED && !g.opts.stream_compaction) {
-            s = b == 0 ? g.local_pixels : -1;   // no compaction: the live count is never formed
+            s = b == 0 ? ctl.cnt[0][0][0] : -1;   // no compaction: the live count is never formed
         } else {
             for (int k = 0; k < NSEG; ++k) s += ctl.cnt[b][k][0];
         }
@@ -1081,6 +1162,8 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
         if (s > 0) out->segments += s;
     }
     out->frames_total = (int64_t)ctl.frames;
+    out->frames_per_pass = g.batch;
+    out->last_pass_frames = ctl.batch;
     for (int b = 0; b <= MAXB; ++b) {
         int64_t cur = 0;
         for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k][0];
@@ -1104,7 +1187,7 @@ int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(need_init());
     if (!out || n < g.local_pixels) return fail(PT_E_INVALID, "output too small");
     HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
-    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels);
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels, 1);
     hipLaunchKernelGGL(k_camera, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g.stream));
@@ -1183,12 +1266,14 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
     RC(set_count(0, (int)n));
     const int ntiles = (int)((n + CTILE - 1) / CTILE);
-    HIPCHK(hipMemset(g.d_status, 0, sizeof(uint64_t) * (size_t)(ntiles + 1)));
     if (ntiles > 0) {
         PathBuf pi = pathbuf(0), po = pathbuf(1);
-        hipLaunchKernelGGL(k_compact, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B, po.C,
-                           (const int*)g.d_alive, staged_count(0), &g.d_ctl->cnt[1][0][0], &g.d_ctl->ticket[0],
-                           g.d_status, 7u);
+        hipLaunchKernelGGL(k_compact_count, dim3(ntiles), dim3(BLOCK), 0, g.stream, (const int*)g.d_alive,
+                           staged_count(0), g.d_tile_cnt);
+        hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, g.stream, (const int*)g.d_tile_cnt,
+                           staged_count(0), g.d_tile_off, &g.d_ctl->cnt[1][0][0]);
+        hipLaunchKernelGGL(k_compact_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B,
+                           po.C, (const int*)g.d_alive, staged_count(0), (const int*)g.d_tile_off);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(g.stream));
@@ -1266,51 +1351,70 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     RC(need_init());
     if (!out || count <= 0) return fail(PT_E_INVALID, "bad arguments");
     memset(out, 0, sizeof(*out));
-    // eager launches, a HIP event after every kernel, no host synchronisation until the end
-    std::vector<hipEvent_t> ev;
-    std::vector<int> kind;
-    std::vector<size_t> frame_start;
-    for (int f = 0; f < count; ++f) {
-        hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, first_iteration + f,
-                           g.local_pixels);
-        if (g.opts.pipeline == PT_PIPELINE_STAGED && g.opts.stream_compaction)
-            HIPCHK(hipMemsetAsync(g.d_status, 0, sizeof(uint64_t) * (size_t)((g.capacity + CTILE - 1) / CTILE + 1),
-                                  g.stream));
-        frame_start.push_back(ev.size());
-        RC(enqueue_frame_body(&ev, &kind));
-        g.frames_done++;
-        g.last_iter = first_iteration + f;
+    // the same passes as pt_trace_frames, launched eagerly with per-dispatch start/stop events,
+    // no host synchronisation until the end; stream-level events around the whole run
+    std::vector<ProfRec> rec;
+    std::vector<size_t> pass_start;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, g.stream));
+    g_prof = &rec;
+    int rc = PT_OK;
+    for (int i = 0; i < count && rc == PT_OK;) {
+        const int f = std::min(g.batch, count - i);
+        pass_start.push_back(rec.size());
+        rc = enqueue_pass(first_iteration + i, f);
+        g.frames_done += f;
+        g.last_iter = first_iteration + i + f - 1;
+        i += f;
     }
-    HIPCHK(hipStreamSynchronize(g.stream));
+    g_prof = nullptr;
+    (void)hipEventRecord(e1, g.stream);
+    hipError_t se = hipStreamSynchronize(g.stream);
+    const int passes = (int)pass_start.size();
     double bounce_ms[MAXB] = {0};
-    double frame_ms = 0, compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0;
-    for (int f = 0; f < count; ++f) {
-        size_t a = frame_start[f], b = (f + 1 < count) ? frame_start[f + 1] : ev.size();
-        float total = 0;
-        (void)hipEventElapsedTime(&total, ev[a], ev[b - 1]);
-        frame_ms += total;
-        int bi = 0;
-        for (size_t i = a + 1; i < b; ++i) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, ev[i - 1], ev[i]);
-            int k = kind[i];
-            if (k >= 100) bounce_ms[k - 100] += ms;
-            else if (k == 0) cam_ms += ms;
-            else if (k == 1) isect_ms += ms;
-            else if (k == 2) shade_ms += ms;
-            else if (k == 3) { compact_ms += ms; if (bi < MAXB) bounce_ms[bi++] += ms; }
-            else if (k == 4) sort_ms += ms;
+    double compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0, scan_ms = 0, comb_ms = 0;
+    float frame_ms = 0;
+    if (rc == PT_OK && se == hipSuccess) {
+        (void)hipEventElapsedTime(&frame_ms, e0, e1);
+        for (int f = 0; f < passes; ++f) {
+            size_t a = pass_start[f], b = (f + 1 < passes) ? pass_start[f + 1] : rec.size();
+            int bi = 0;
+            for (size_t i = a; i < b; ++i) {
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, rec[i].start, rec[i].stop);
+                int k = rec[i].kind;
+                if (k >= 100) bounce_ms[k - 100] += ms;
+                else if (k == 0) cam_ms += ms;
+                else if (k == 1) isect_ms += ms;
+                else if (k == 2) shade_ms += ms;
+                else if (k == 3) { compact_ms += ms; if (bi < MAXB) bounce_ms[bi++] += ms; }
+                else if (k == 5) scan_ms += ms;
+                else if (k == 4) sort_ms += ms;
+                else if (k == 6) comb_ms += ms;
+            }
         }
     }
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    for (auto& r : rec) {
+        (void)hipEventDestroy(r.start);
+        (void)hipEventDestroy(r.stop);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    RC(rc);
+    HIPCHK(se);
     out->frames = count;
-    out->frame_ms = (float)(frame_ms / count);
-    for (int b = 0; b < MAXB; ++b) out->bounce_ms[b] = (float)(bounce_ms[b] / count);
+    out->passes = passes;
+    out->frame_ms = frame_ms / count;
+    for (int b = 0; b < MAXB; ++b) out->bounce_ms[b] = (float)(bounce_ms[b] / passes);
+    out->combine_ms = (float)(comb_ms / count);
     out->compact_ms = (float)(compact_ms / count);
     out->intersect_ms = (float)(isect_ms / count);
     out->shade_ms = (float)(shade_ms / count);
     out->camera_ms = (float)(cam_ms / count);
     out->sort_ms = (float)(sort_ms / count);
+    out->compact_scan_ms = (float)(scan_ms / count);
     return PT_OK;
 }
 

@@ -56,7 +56,7 @@ class PtError(RuntimeError):
 class _Options(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "stream_compaction", "material_sort", "bvh", "arg_order", "pipeline", "use_graph", "device",
-        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size", "variant")]
+        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size", "variant", "frames_per_pass")]
 
 
 class _SceneView(ctypes.Structure):
@@ -72,14 +72,16 @@ class _SceneView(ctypes.Structure):
 class _FrameStats(ctypes.Structure):
     _fields_ = [("iteration", ctypes.c_int32), ("bounces", ctypes.c_int32), ("live", ctypes.c_int64 * 64),
                 ("segments", ctypes.c_int64), ("pixels", ctypes.c_int64), ("frames_total", ctypes.c_int64),
-                ("live_total", ctypes.c_int64 * 65), ("segments_total", ctypes.c_int64)]
+                ("live_total", ctypes.c_int64 * 65), ("segments_total", ctypes.c_int64),
+                ("frames_per_pass", ctypes.c_int32), ("last_pass_frames", ctypes.c_int32)]
 
 
 class _KernelTimes(ctypes.Structure):
     _fields_ = [("frames", ctypes.c_int32), ("frame_ms", ctypes.c_float), ("bounce_ms", ctypes.c_float * 64),
                 ("compact_ms", ctypes.c_float), ("intersect_ms", ctypes.c_float), ("shade_ms", ctypes.c_float),
                 ("camera_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("compact_bytes", ctypes.c_int64),
-                ("frame_bytes", ctypes.c_int64)]
+                ("frame_bytes", ctypes.c_int64), ("compact_scan_ms", ctypes.c_float), ("passes", ctypes.c_int32),
+                ("combine_ms", ctypes.c_float)]
 
 
 # every symbol the C-ABI header declares (tests check the library exports all of them)
@@ -282,7 +284,8 @@ class PathTracer:
         return {"iteration": s.iteration, "live": [s.live[i] for i in range(s.bounces)],
                 "segments": s.segments, "pixels": s.pixels, "frames_total": s.frames_total,
                 "live_total": [s.live_total[i] for i in range(s.bounces + 1)],
-                "segments_total": s.segments_total}
+                "segments_total": s.segments_total, "frames_per_pass": s.frames_per_pass,
+                "last_pass_frames": s.last_pass_frames}
 
     def reset_stats(self):
         _check(lib.pt_reset_stats(), "pt_reset_stats")
@@ -291,10 +294,10 @@ class PathTracer:
         t = _KernelTimes()
         _check(lib.pt_profile_frames(int(first_iteration), int(count), ctypes.byref(t)), "pt_profile_frames")
         self.iteration = first_iteration + count - 1
-        return {"frames": t.frames, "frame_ms": t.frame_ms,
+        return {"frames": t.frames, "passes": t.passes, "frame_ms": t.frame_ms, "combine_ms": t.combine_ms,
                 "bounce_ms": [t.bounce_ms[i] for i in range(max(1, self.trace_depth))],
                 "compact_ms": t.compact_ms, "intersect_ms": t.intersect_ms, "shade_ms": t.shade_ms,
-                "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_bytes": t.compact_bytes}
+                "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms}
 
     # ---- single-kernel entry points (tests) ----
     def test_camera(self, iteration: int) -> np.ndarray:

@@ -2,8 +2,9 @@
 CPU for tests).  The reference is single-GPU (main.cpp:174); pixels are independent (the RNG
 is keyed by pixel index, pathtrace.cu:54), so a frame shards without any data-path exchange:
 
-* SAMPLES (weak scaling): rank r traces iterations r+1, r+1+W, ...  of the whole frame; the
-  accumulated images are summed once per reported frame.  Sum order differs from one GPU, so the
+* SAMPLES (weak scaling): rank r traces a contiguous block of iterations of the whole frame
+  (contiguous so pt_trace_frames groups them into multi-frame passes); the accumulated images
+  are summed once per reported frame.  Sum order differs from one GPU, so the
   combined image equals the single-GPU one to float rounding of the final sum (not bit-wise).
 * PIXELS (strong scaling): rank r traces every iteration for its interleaved row bands
   ((y // rows) % W == r), zeros elsewhere; the sum is exact (x + 0 == x), bit-identical to
@@ -32,8 +33,8 @@ def local_to_pixel(local: np.ndarray, width: int, rows: int, world: int, rank: i
 
 
 def sample_iterations(steps: int, world: int, rank: int, first: int = 1) -> list:
-    """Iterations traced by `rank` for `steps` local frames in SAMPLES mode."""
-    return [first + rank + k * world for k in range(steps)]
+    """Iterations traced by `rank` for `steps` local frames in SAMPLES mode (a contiguous block)."""
+    return [first + rank * steps + k for k in range(steps)]
 
 
 def combine(image, dst: int = 0, group=None):
@@ -61,9 +62,9 @@ def render(scene_path: str, spp: int, mode: str = "pixels", res=None, depth=None
         tr.trace_frames(1, spp)
     elif mode == "samples":
         tr = ptamd.PathTracer(sc, device=dev, **options)
-        for it in sample_iterations(-(-spp // world), world, rank):
-            if it <= spp:
-                tr.trace_frames(it, 1)
+        its = [it for it in sample_iterations(-(-spp // world), world, rank) if it <= spp]
+        if its:
+            tr.trace_frames(its[0], len(its))
     else:
         raise ValueError(mode)
     tr.synchronize()

@@ -195,6 +195,58 @@ def test_frames_bitexact(name, res, depth, opts, oracle, ptamd):
     tr.free()
 
 
+PASS_CASES = [
+    ("cornell", (64, 64), None, {}, 2),
+    ("cornell", (64, 64), None, {}, 4),
+    ("cornell", (64, 64), None, {"pipeline": 1}, 3),
+    ("cornell", (64, 64), None, {"pipeline": 1, "stream_compaction": 0}, 4),
+    ("cornell_glass_test", (64, 64), None, {"pipeline": 1, "material_sort": 1}, 2),
+    ("cornell_glass_test", (48, 40), None, {"use_graph": 0}, 5),
+    ("cornell_obj_bnnuy", (48, 48), None, {}, 0),
+    ("cornell_obj_khaslana", (32, 32), 12, {"pipeline": 1}, 16),
+    ("cornell", (40, 30), 0, {}, 3),
+    ("cornell_microfacet_test", (50, 50), None, {"shard_mode": 1, "shard_rank": 1, "shard_count": 2}, 4),
+]
+
+
+@pytest.mark.parametrize("name,res,depth,opts,fpp", PASS_CASES)
+def test_multi_frame_passes_bitexact(name, res, depth, opts, fpp, oracle, ptamd):
+    """pt_trace_frames traces F frames per wavefront pass (frames_per_pass; 0 = auto); the image
+    after 5 frames (passes F, F, ..., remainder) equals 5 sequential oracle frames bit-for-bit,
+    and the device path-segment counters equal the oracle's."""
+    a, b = _oracle_pair(oracle, ptamd, name, res, depth)
+    tr = ptamd.PathTracer(b, frames_per_pass=fpp, **opts)
+    r = oracle.Renderer(a, oracle.options(stream_compaction=opts.get("stream_compaction", 1),
+                                          material_sort=opts.get("material_sort", 0), **BIT))
+    segs = 0
+    for it in range(1, 6):
+        live = r.trace(it)
+        segs += int(np.maximum(live, 0).sum()) if a.trace_depth > 0 else 0
+    tr.trace_frames(1, 5)
+    st = tr.stats()
+    assert st["frames_total"] == 5
+    img = tr.image()
+    want = r.image
+    if opts.get("shard_mode") == 1:                 # only this shard's rows are traced
+        from ptamd import dist as D
+        w, h = res
+        mask = np.zeros(h, bool)
+        mask[D.owned_rows(h, 8, opts["shard_count"], opts["shard_rank"])] = True
+        want = want.copy()
+        want[~np.repeat(mask, w)] = 0.0
+    elif opts.get("stream_compaction", 1) and a.trace_depth > 0:
+        assert st["segments_total"] == segs
+    assert _eq(img, want), (name, fpp, int(np.sum(img.view(np.uint32) != want.view(np.uint32))))
+    # the profiling path groups frames the same way and traces the same image
+    p = tr.profile(6, 3)
+    assert p["frames"] == 3
+    for it in range(6, 9):
+        r.trace(it)
+    if opts.get("shard_mode") != 1:
+        assert _eq(tr.image(), r.image)
+    tr.free()
+
+
 def test_full_resolution_cornell(oracle, ptamd):
     """BASELINE config 2 (800x800, depth 8): fused == staged == oracle, live counts included."""
     a, b = _oracle_pair(oracle, ptamd, "cornell", None)

@@ -23,25 +23,26 @@ def main():
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", default="")
     ap.add_argument("--pipeline", type=int, default=0)
+    ap.add_argument("--fpp", default="0", help="frames_per_pass values to A/B (0 = auto)")
     args = ap.parse_args()
     import ptamd
     res = tuple(int(x) for x in args.res.split("x")) if args.res else None
     sc = ptamd.SceneFile(os.path.join(REPO, "scenes", args.scene + ".json"), res=res)
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = [(int(v), int(f)) for v in args.variants.split(",") for f in args.fpp.split(",")]
     times = {v: [] for v in variants}
     kern = {v: [] for v in variants}
     ref = None
     for r in range(args.rounds):
         for v in variants:
-            tr = ptamd.PathTracer(sc, variant=v, pipeline=args.pipeline)
+            tr = ptamd.PathTracer(sc, variant=v[0], frames_per_pass=v[1], pipeline=args.pipeline)
             tr.trace_frames(1, 3)
             tr.synchronize()
             t0 = time.perf_counter()
             tr.trace_frames(4, args.frames)
             tr.synchronize()
             times[v].append((time.perf_counter() - t0) / args.frames * 1e3)
-            p = tr.profile(4 + args.frames, 5)
-            kern[v].append(p["bounce_ms"])
+            p = tr.profile(4 + args.frames, 16)
+            kern[v].append(p["bounce_ms"] + [p["frame_ms"], p["combine_ms"]])
             img = tr.image()
             if ref is None:
                 ref = img
@@ -49,8 +50,8 @@ def main():
             tr.free()
     out = {}
     for v in variants:
-        out[v] = {"ms_per_frame_median": float(np.median(times[v])), "ms_per_frame_min": float(np.min(times[v])),
-                  "bounce_ms_median": [round(float(x), 4) for x in np.median(np.array(kern[v]), axis=0)]}
+        out[f"var{v[0]}_fpp{v[1]}"] = {"ms_per_frame_median": float(np.median(times[v])), "ms_per_frame_min": float(np.min(times[v])),
+                  "per_launch_bounce_ms_then_frame_ms_combine_ms": [round(float(x), 4) for x in np.median(np.array(kern[v]), axis=0)]}
     print(json.dumps({"scene": args.scene, "frames": args.frames, "rounds": args.rounds, "results": out}, indent=1))
 
 
