@@ -189,6 +189,12 @@ typedef struct pt_kernel_times {
  * per frame.  Frames are grouped into passes exactly as pt_trace_frames groups them. */
 int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_times* out);
 
+/* Tools: counters filled by the fused kernel when pt_options.variant has bit 4 (section timing):
+ * [0..5] shader-clock cycles per section summed over waves (load, cull, exact tests, hit finish,
+ * shade, gather+compact+store), [6] exact geom tests, [7] candidates, [8] candidate-loop
+ * iterations (per wave), [9] waves, [10] live lanes.  `reset` zeroes them after the read. */
+int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset);
+
 #ifdef __cplusplus
 }
 #endif

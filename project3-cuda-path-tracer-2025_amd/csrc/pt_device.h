@@ -96,8 +96,8 @@ struct DevGeom {
     float inv[12];
     float fwd[12];
     float itr[12];
-    float box_c[3];
-    float box_h[3];
+    float box_lo[3];    // conservative world box (outward-rounded, margin included)
+    float box_hi[3];
     int32_t type;
     int32_t materialid;
     int32_t _pad[4];
@@ -177,53 +177,53 @@ PT_DEV float u01(Rng& r) { return (float)(rng_next(r) - 1u) * 4.6566128730773925
 // getPointOnRay, intersections.h:29-32
 PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize(d); }
 
-// boxIntersectionTest, intersections.cu:3-57.  Returns t; `seed` receives the object-space
-// normal (tmin_n) the winner's world normal is derived from.
-PT_DEV float box_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
-    f3 qo = xform(g.inv, ro, 1.0f);
-    f3 qd = normalize(xform(g.inv, rd, 0.0f));
-    float tmin = -1e38f, tmax = 1e38f;
-    f3 tmin_n = mk(0.f, 0.f, 0.f), tmax_n = mk(0.f, 0.f, 0.f);
+// boxIntersectionTest (intersections.cu:3-57) and sphereIntersectionTest (intersections.cu:
+// 59-109) as ONE routine: both start by taking the ray to object space (q.origin, normalized
+// q.direction) and end with the world hit point's distance, so a wave whose lanes test a mix of
+// cubes and spheres runs the shared prologue/epilogue once and diverges only in the middle.
+// Every float operation and its order is the reference's.  Returns t (-1 on miss); `seed`
+// receives what the winner's normal is derived from: the box's object-space face normal
+// (tmin_n), or the sphere's object-space hit point.
+PT_DEV float geom_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
+    const f3 qo = xform(g.inv, ro, 1.0f);
+    const f3 qd = normalize(xform(g.inv, rd, 0.0f));
+    bool hit;
+    float tq;
+    f3 s = mk(0.f, 0.f, 0.f);
+    if (g.type == PT_CUBE) {
+        float tmin = -1e38f, tmax = 1e38f;
+        f3 tmin_n = mk(0.f, 0.f, 0.f), tmax_n = mk(0.f, 0.f, 0.f);
 #pragma unroll
-    for (int xyz = 0; xyz < 3; ++xyz) {
-        float qdx = comp(qd, xyz), qox = comp(qo, xyz);
-        float t1 = (-0.5f - qox) / qdx;
-        float t2 = (+0.5f - qox) / qdx;
-        float ta = gmin(t1, t2);
-        float tb = gmax(t1, t2);
-        float s = t2 < t1 ? +1.0f : -1.0f;
-        f3 n = mk(xyz == 0 ? s : 0.f, xyz == 1 ? s : 0.f, xyz == 2 ? s : 0.f);
-        if (ta > 0 && ta > tmin) { tmin = ta; tmin_n = n; }
-        if (tb < tmax) { tmax = tb; tmax_n = n; }
-    }
-    if (tmax >= tmin && tmax > 0) {
+        for (int xyz = 0; xyz < 3; ++xyz) {
+            float qdx = comp(qd, xyz), qox = comp(qo, xyz);
+            float t1 = (-0.5f - qox) / qdx;
+            float t2 = (+0.5f - qox) / qdx;
+            float ta = gmin(t1, t2);
+            float tb = gmax(t1, t2);
+            float sg = t2 < t1 ? +1.0f : -1.0f;
+            f3 n = mk(xyz == 0 ? sg : 0.f, xyz == 1 ? sg : 0.f, xyz == 2 ? sg : 0.f);
+            if (ta > 0 && ta > tmin) { tmin = ta; tmin_n = n; }
+            if (tb < tmax) { tmax = tb; tmax_n = n; }
+        }
+        hit = tmax >= tmin && tmax > 0;
         if (tmin <= 0) { tmin = tmax; tmin_n = tmax_n; }
-        f3 p = xform(g.fwd, point_on_ray(qo, qd, tmin), 1.0f);
-        seed = tmin_n;
-        return length(ro - p);
+        tq = tmin;
+        s = tmin_n;
+    } else {
+        float vDotDirection = dot(qo, qd);
+        float radicand = vDotDirection * vDotDirection - (dot(qo, qo) - 0.25f);   // powf(.5, 2) == .25
+        float squareRoot = __builtin_sqrtf(radicand);
+        float firstTerm = -vDotDirection;
+        float t1 = firstTerm + squareRoot;
+        float t2 = firstTerm - squareRoot;
+        hit = !(radicand < 0) && !(t1 < 0 && t2 < 0);
+        tq = (t1 > 0 && t2 > 0) ? gmin(t1, t2) : gmax(t1, t2);
     }
-    return -1.0f;
-}
-
-// sphereIntersectionTest, intersections.cu:59-109.  `seed` = object-space hit point.
-PT_DEV float sphere_test(const DevGeom& g, f3 ro_w, f3 rd_w, f3& seed) {
-    f3 ro = xform(g.inv, ro_w, 1.0f);
-    f3 rd = normalize(xform(g.inv, rd_w, 0.0f));
-    float vDotDirection = dot(ro, rd);
-    float radicand = vDotDirection * vDotDirection - (dot(ro, ro) - 0.25f);  // powf(.5, 2) == .25
-    if (radicand < 0) return -1.0f;
-    float squareRoot = __builtin_sqrtf(radicand);
-    float firstTerm = -vDotDirection;
-    float t1 = firstTerm + squareRoot;
-    float t2 = firstTerm - squareRoot;
-    float t;
-    if (t1 < 0 && t2 < 0) return -1.0f;
-    else if (t1 > 0 && t2 > 0) t = gmin(t1, t2);
-    else t = gmax(t1, t2);
-    f3 objp = point_on_ray(ro, rd, t);
-    f3 p = xform(g.fwd, objp, 1.0f);
-    seed = objp;
-    return length(ro_w - p);
+    if (!hit) return -1.0f;
+    const f3 objp = point_on_ray(qo, qd, tq);
+    const f3 p = xform(g.fwd, objp, 1.0f);
+    seed = g.type == PT_CUBE ? s : objp;
+    return length(ro - p);
 }
 
 // Moller-Trumbore, intersections.cu:112-145

@@ -12,7 +12,8 @@
 
 namespace ptd {
 
-constexpr int NSEG = 8;        // output segments of the fused compaction (one per XCD group)
+constexpr int NSEG = 8;
+constexpr int LDS_GEOMS = 64;  // fused kernel: geom tables up to this size are staged in LDS        // output segments of the fused compaction (one per XCD group)
 constexpr int MAXB = 64;       // max trace depth supported by the frame control block
 constexpr int BLOCK = 256;     // threads per block of the per-path kernels
 constexpr int MAXSTACK = 64;   // reference BVH stack (intersections.cu:167)
@@ -22,6 +23,8 @@ constexpr int CNT_PAD = 32;    // one 128-byte cache line per live counter (atom
 enum : int {
     VAR_WAVE_ATOMIC = 1,   // compaction: one atomic per wave, no block barrier
     VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
+    VAR_SECTION_TIMING = 4,
+    VAR_OCC8 = 8,          // fused kernel compiled for 8 waves/SIMD (<= 64 VGPRs)// tools only: per-wave shader-clock section times into g_sections
 };
 
 struct CamDev {
@@ -60,6 +63,25 @@ struct FrameCtl {
     int ticket[MAXB];                       // dynamic tile ids of the staged compaction kernel
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
 };
+
+// VAR_SECTION_TIMING (tools/section_times.py): wave-level s_memtime deltas per kernel section and
+// per-lane work counters, summed by the first active lane of each wave
+enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
+       SEC_N_WAVES, SEC_N_LANES, SEC_COUNT };
+__device__ unsigned long long g_sections[16];
+PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
+PT_DEV void sec_add(int k, uint64_t v) {
+    // one atomic per wave: the first active lane adds the wave's value
+    if (__builtin_amdgcn_read_exec() == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int first = __builtin_ctzll(__builtin_amdgcn_read_exec());
+    if (lane == first) atomicAdd(&g_sections[k], (unsigned long long)v);
+}
+PT_DEV void sec_add_lanes(int k, int v) {    // sum over the wave's active lanes
+    int s = v;
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    sec_add(k, (uint64_t)s);
+}
 
 // a wavefront of paths: three float4 streams
 struct PathBuf {
@@ -174,29 +196,43 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
 
 // Conservative pre-test of one geom (approximate arithmetic, never decides a result): true
 // when the exact test is CERTAIN not to update (t_min, winner) — the ray line misses the geom's
-// margin-expanded world box, or enters it farther than t_min.  NaN anywhere: never skips.
-PT_DEV bool cull_geom(const DevGeom& g, f3 ro, f3 invd, float rdlen, float t_min) {
-    float t0 = -1e-2f, t1 = FLT_MAX_;
-    bool nan = false;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        float o = comp(ro, k) - g.box_c[k];
-        float id = comp(invd, k);
-        float ta = (-g.box_h[k] - o) * id;
-        float tb = (g.box_h[k] - o) * id;
-        nan |= (ta != ta) | (tb != tb);
-        t0 = __builtin_fmaxf(t0, __builtin_fminf(ta, tb));
-        t1 = __builtin_fminf(t1, __builtin_fmaxf(ta, tb));
-    }
-    if (nan || rdlen != rdlen) return false;
-    if (t1 < t0) return true;                                       // certain miss
-    return t0 > 0.0f && t0 * rdlen * (1.0f - 1e-5f) - 1e-4f > t_min;  // certainly farther
+// margin-expanded world box, or enters it farther than t_min.  Slabs as fma(bound, 1/d, -o/d)
+// with 1/d clamped to +-1e20 (finite inputs never make a NaN).  A NaN or infinite ray skips
+// everything, which is what its exact tests return too: a NaN/inf distance never wins
+// (`t > 0 && t_min > t`).
+struct CullRay {
+    f3 id;       // clamped approximate 1 / direction
+    f3 rid;      // origin * id
+    float rdlen;
+};
+PT_DEV float clamp_inv(float x) {
+    return __builtin_fminf(__builtin_fmaxf(__builtin_amdgcn_rcpf(x), -1e20f), 1e20f);
+}
+PT_DEV CullRay cull_ray(f3 ro, f3 rd) {
+    CullRay c;
+    c.id = mk(clamp_inv(rd.x), clamp_inv(rd.y), clamp_inv(rd.z));
+    c.rid = mk(ro.x * c.id.x, ro.y * c.id.y, ro.z * c.id.z);
+    c.rdlen = __builtin_amdgcn_sqrtf(__builtin_fmaf(rd.x, rd.x, __builtin_fmaf(rd.y, rd.y, rd.z * rd.z)));
+    return c;
+}
+template <bool FARTHER = true>
+PT_DEV bool cull_geom(const DevGeom& g, const CullRay& c, float t_min) {
+    const float a0 = __builtin_fmaf(g.box_lo[0], c.id.x, -c.rid.x), b0 = __builtin_fmaf(g.box_hi[0], c.id.x, -c.rid.x);
+    const float a1 = __builtin_fmaf(g.box_lo[1], c.id.y, -c.rid.y), b1 = __builtin_fmaf(g.box_hi[1], c.id.y, -c.rid.y);
+    const float a2 = __builtin_fmaf(g.box_lo[2], c.id.z, -c.rid.z), b2 = __builtin_fmaf(g.box_hi[2], c.id.z, -c.rid.z);
+    const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                     __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
+    const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                     __builtin_fmaxf(a2, b2));
+    if (!(t1 >= t0)) return true;                                   // certain miss (or NaN ray)
+    return FARTHER && t0 > 0.0f && t0 * c.rdlen * (1.0f - 1e-5f) - 1e-4f > t_min;  // certainly farther
 }
 
 // winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
 // miss / facing conventions of pathtrace.cu:397-446
 template <bool HAS_BVH>
-PT_DEV Hit finish_hit(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_min, int win, f3 seed) {
+PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
+                      f3 seed) {
     Hit h;
     h.tri = -1;
     h.u = 0.f;
@@ -205,7 +241,7 @@ PT_DEV Hit finish_hit(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_min,
     int hit_index = -1;   // reference hit_geom_index: prim -> its materialid, mesh -> -2
     int mat = 0;
     if (win >= 0) {
-        const DevGeom& g = sc.geoms[win];
+        const DevGeom& g = geoms[win];
         normal = normalize(xform(g.itr, seed, 0.0f));
         hit_index = g.materialid;
         mat = g.materialid;
@@ -261,20 +297,19 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
     float t_min = FLT_MAX_;
     int win = -1;
     f3 seed = mk(0.f, 0.f, 0.f);
-    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+    const CullRay cr = cull_ray(ro, rd);
     for (int i = 0; i < sc.num_geoms; ++i) {
         const DevGeom& g = sc.geoms[i];
-        if (cull_geom(g, ro, invd, rdlen, t_min)) continue;
+        if (cull_geom(g, cr, t_min)) continue;
         f3 s;
-        float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
+        float t = geom_test(g, ro, rd, s);
         if (t > 0.0f && t_min > t) {
             t_min = t;
             win = i;
             seed = s;
         }
     }
-    return finish_hit<HAS_BVH>(sc, ro, rd, stack, t_min, win, seed);
+    return finish_hit<HAS_BVH>(sc, sc.geoms, ro, rd, stack, t_min, win, seed);
 }
 
 // computeIntersections with the exact per-geom tests driven by a per-lane candidate queue:
@@ -282,25 +317,35 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
 // pop ITS next candidate (increasing geom index, so the first-minimum tie rule is unchanged)
 // and re-checks the cull against its current t_min before the exact test.  The wave executes
 // max-over-lanes(candidates) exact tests instead of one per geom any lane needs.
-template <bool HAS_BVH>
-PT_DEV Hit intersect_scene_q(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
-    if (sc.num_geoms > 64) return intersect_scene<HAS_BVH>(sc, ro, rd, stack);
-    const f3 invd = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-    const float rdlen = __builtin_amdgcn_sqrtf(rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+// `lgeoms`: the block's LDS copy of the geom table (the caller's job; sc.num_geoms <= 64).
+template <bool HAS_BVH, bool TIMING = false>
+PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
+    uint64_t tc0 = TIMING ? sec_clock() : 0;
+    const CullRay cr = cull_ray(ro, rd);
     uint64_t cand = 0;
+#pragma unroll 4
     for (int i = 0; i < sc.num_geoms; ++i)
-        if (!cull_geom(sc.geoms[i], ro, invd, rdlen, FLT_MAX_)) cand |= 1ull << i;
+        if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
     float t_min = FLT_MAX_;
     int win = -1;
     f3 seed = mk(0.f, 0.f, 0.f);
+    int n_exact = 0, n_iters = 0;
+    uint64_t tc1 = 0;
+    if (TIMING) {
+        tc1 = sec_clock();
+        sec_add(SEC_CULL, tc1 - tc0);
+        sec_add_lanes(SEC_N_CAND, __builtin_popcountll(cand));
+    }
     while (__any(cand != 0)) {
+        if (TIMING) n_iters++;
         if (cand != 0) {
             const int i = __builtin_ctzll(cand);
             cand &= cand - 1;
-            const DevGeom& g = sc.geoms[i];
-            if (!cull_geom(g, ro, invd, rdlen, t_min)) {
+            const DevGeom& g = lgeoms[i];
+            if (!cull_geom(g, cr, t_min)) {
                 f3 s;
-                float t = (g.type == PT_CUBE) ? box_test(g, ro, rd, s) : sphere_test(g, ro, rd, s);
+                if (TIMING) n_exact++;
+                float t = geom_test(g, ro, rd, s);
                 if (t > 0.0f && t_min > t) {
                     t_min = t;
                     win = i;
@@ -309,7 +354,16 @@ PT_DEV Hit intersect_scene_q(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
             }
         }
     }
-    return finish_hit<HAS_BVH>(sc, ro, rd, stack, t_min, win, seed);
+    if (TIMING) {
+        uint64_t tc2 = sec_clock();
+        sec_add(SEC_EXACT, tc2 - tc1);
+        sec_add_lanes(SEC_N_EXACT, n_exact);
+        sec_add(SEC_N_ITERS, (uint64_t)n_iters);
+        Hit h = finish_hit<HAS_BVH>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
+        sec_add(SEC_FINISH, sec_clock() - tc2);
+        return h;
+    }
+    return finish_hit<HAS_BVH>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
 }
 
 // kernShadeMaterialProper for one live path (pathtrace.cu:521-621).  Textures: a material

@@ -111,9 +111,11 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
 // FUSED: camera (bounce 0) | load -> intersect -> shade -> gather dead -> compact survivors
 // --------------------------------------------------------------------------------------------
 template <bool FIRST, bool HAS_BVH, int VAR>
-__global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu((VAR & VAR_OCC8) ? 8 : 1))) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride) {
-    extern __shared__ int s_stack[];   // HAS_BVH: stack_depth x BLOCK ints
+    // dynamic LDS: [geom table, sc.num_geoms <= LDS_GEOMS, candidate-queue variants]
+    //              [HAS_BVH: traversal stack, stack_depth x BLOCK ints]
+    extern __shared__ float4 s_dyn[];
     __shared__ int s_wave[BLOCK / 64];
     __shared__ int s_base;
     const int iter = ctl->iter;
@@ -130,7 +132,18 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     }
     const int block_start = blockIdx.x * BLOCK;
     if (block_start >= n) return;
+    constexpr bool TIMING = (VAR & VAR_SECTION_TIMING) != 0;
+    constexpr bool QUEUE = (VAR & VAR_CAND_QUEUE) != 0;
+    uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
+    const bool lds_geoms = QUEUE && sc.num_geoms <= LDS_GEOMS;
+    DevGeom* s_geoms = reinterpret_cast<DevGeom*>(s_dyn);
+    int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? sc.num_geoms * (int)(sizeof(DevGeom) / 16) : 0));
+    if (lds_geoms) {   // per-lane candidate tests then read their geom from LDS, not L2
+        const float4* src = reinterpret_cast<const float4*>(sc.geoms);
+        for (int k = tid; k < sc.num_geoms * (int)(sizeof(DevGeom) / 16); k += BLOCK) s_dyn[k] = src[k];
+        __syncthreads();
+    }
     const int gid = block_start + tid;
     const bool active = gid < n;
     PathReg p;
@@ -146,15 +159,27 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             for (int k = 1; k < NSEG; ++k) s += (gid >= segoff[k]) ? 1 : 0;
             p = load_path(in, s * seg_stride + (gid - segoff[s]));
         }
-        if (p.rb > 0) {
-            Hit h = (VAR & VAR_CAND_QUEUE) ? intersect_scene_q<HAS_BVH>(sc, p.o, p.d, s_stack + tid)
-                                           : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
-            shade_path(sc, p, h, iter + p.slot);
+        if (TIMING) {
+            __builtin_amdgcn_s_waitcnt(0);
+            uint64_t t = sec_clock();
+            sec_add(SEC_LOAD, t - tc);
+            sec_add(SEC_N_WAVES, 1);
+            sec_add_lanes(SEC_N_LANES, p.rb > 0 ? 1 : 0);
         }
+        if (p.rb > 0) {
+            Hit h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING>(sc, s_geoms, p.o, p.d, s_stack + tid)
+                              : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
+            uint64_t ts = TIMING ? sec_clock() : 0;
+            shade_path(sc, p, h, iter + p.slot);
+            if (TIMING) {
+                tc = sec_clock();
+                sec_add(SEC_SHADE, tc - ts);
+            }
+        }
+        if (TIMING) tc = sec_clock();
     }
     const bool surv = active && p.rb > 0;
     if (active && !surv) gather_into_image(image, sc, batch, p);
-
     const uint64_t m = __ballot(surv);
     const int lane = tid & 63, w = tid >> 6;
     const int seg = blockIdx.x & (NSEG - 1);
@@ -182,6 +207,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     }
     __syncthreads();
     if (surv) store_path(out, s_base + s_wave[w] + mbcnt(m), p);
+    if (TIMING && active) sec_add(SEC_STORE, sec_clock() - tc);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -590,7 +616,8 @@ const int* staged_count(int b) { return &g.d_ctl->cnt[b][0][0]; }
 
 template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
-    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), HAS_BVH ? g.bvh_lds : 0, g.sc, in, out,
+    const size_t geom_lds = (VAR & VAR_CAND_QUEUE) && g.sc.num_geoms <= LDS_GEOMS ? sizeof(DevGeom) * g.sc.num_geoms : 0;
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + (HAS_BVH ? g.bvh_lds : 0), g.sc, in, out,
            g.d_ctl, g.d_image, b, g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
@@ -599,6 +626,9 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 0: launch_bounce_t<FIRST, HAS_BVH, 0>(grid, in, out, b); break;
         case 1: launch_bounce_t<FIRST, HAS_BVH, 1>(grid, in, out, b); break;
         case 2: launch_bounce_t<FIRST, HAS_BVH, 2>(grid, in, out, b); break;
+        case 6: launch_bounce_t<FIRST, HAS_BVH, 6>(grid, in, out, b); break;
+        case 10: launch_bounce_t<FIRST, HAS_BVH, 10>(grid, in, out, b); break;
+        case 11: launch_bounce_t<FIRST, HAS_BVH, 11>(grid, in, out, b); break;
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -622,7 +652,7 @@ int enqueue_pass_body(int batch) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 3, dim3(nb), in, out, b);
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 15, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -926,20 +956,54 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             }
         d.type = gg.type;
         d.materialid = gg.materialid;
-        // world box of the transformed unit cube (contains the radius-0.5 sphere too), grown by
-        // a margin far above every rounding the exact test can make: 1e-3 of the largest half
-        // extent + 1e-3 absolute (object-space pull-back 1e-4 times the scale)
-        float hmax = 0.f;
-        for (int r = 0; r < 3; ++r) {
-            d.box_c[r] = d.fwd[9 + r];
-            d.box_h[r] = 0.5f * (std::fabs(d.fwd[r]) + std::fabs(d.fwd[3 + r]) + std::fabs(d.fwd[6 + r]));
-            hmax = std::max(hmax, d.box_h[r]);
+    }
+    // conservative world boxes for cull_geom: the transformed unit cube (contains the radius-0.5
+    // sphere too), grown by a margin far above every rounding the exact test can make (1e-3 of
+    // the largest half extent + 1e-3 absolute; object-space pull-back is 1e-4 times the scale)
+    // and above the cull's own fma/rcp error for ray origins anywhere in the scene (1e-6 of the
+    // scene extent), then rounded outward.
+    {
+        double extent = std::max({std::fabs((double)s->camera.position.x), std::fabs((double)s->camera.position.y),
+                                  std::fabs((double)s->camera.position.z), 1.0});
+        std::vector<float> bc(3 * (size_t)s->num_geoms), bh(3 * (size_t)s->num_geoms);
+        std::vector<char> fin(s->num_geoms);
+        for (int i = 0; i < s->num_geoms; ++i) {
+            DevGeom& d = geoms[i];
+            float hmax = 0.f;
+            for (int r = 0; r < 3; ++r) {
+                bc[3 * i + r] = d.fwd[9 + r];
+                bh[3 * i + r] = 0.5f * (std::fabs(d.fwd[r]) + std::fabs(d.fwd[3 + r]) + std::fabs(d.fwd[6 + r]));
+                hmax = std::max(hmax, bh[3 * i + r]);
+            }
+            for (int r = 0; r < 3; ++r) bh[3 * i + r] += 1e-3f * hmax + 1e-3f * std::max(1.0f, hmax);
+            fin[i] = std::isfinite(hmax) && std::isfinite(bc[3 * i]) && std::isfinite(bc[3 * i + 1]) &&
+                     std::isfinite(bc[3 * i + 2]) && hmax < 1e17f;
+            if (fin[i])
+                for (int r = 0; r < 3; ++r)
+                    extent = std::max(extent, std::fabs((double)bc[3 * i + r]) + (double)bh[3 * i + r]);
         }
-        for (int r = 0; r < 3; ++r) d.box_h[r] += 1e-3f * hmax + 1e-3f * std::max(1.0f, hmax);
-        bool finite = std::isfinite(hmax) && std::isfinite(d.box_c[0]) && std::isfinite(d.box_c[1]) &&
-                      std::isfinite(d.box_c[2]);
-        if (!finite)   // degenerate transform: a box that never culls
-            for (int r = 0; r < 3; ++r) { d.box_c[r] = 0.f; d.box_h[r] = 3.0e38f; }
+        for (int t = 0; t < s->num_triangles; ++t) {
+            const pt_vertex* v[3] = {&s->triangles[t].v1, &s->triangles[t].v2, &s->triangles[t].v3};
+            for (auto* x : v) {
+                double m = std::max({std::fabs((double)x->position.x), std::fabs((double)x->position.y),
+                                     std::fabs((double)x->position.z)});
+                if (std::isfinite(m)) extent = std::max(extent, m);
+            }
+        }
+        const float emargin = (float)std::min(1e-6 * extent, 1e17);
+        for (int i = 0; i < s->num_geoms; ++i) {
+            DevGeom& d = geoms[i];
+            for (int r = 0; r < 3; ++r) {
+                if (!fin[i]) {   // degenerate transform: a box that never culls
+                    d.box_lo[r] = -1e18f;
+                    d.box_hi[r] = 1e18f;
+                    continue;
+                }
+                const float h = bh[3 * i + r] + emargin;
+                d.box_lo[r] = std::nextafter(bc[3 * i + r] - h, -INFINITY);
+                d.box_hi[r] = std::nextafter(bc[3 * i + r] + h, INFINITY);
+            }
+        }
     }
     std::vector<DevMaterial> mats(std::max(1, s->num_materials));
     for (int i = 0; i < s->num_materials; ++i) {
@@ -1344,6 +1408,20 @@ int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4*
     HIPCHK(hipMemcpy(pbo, d_pbo, sizeof(pt_uchar4) * n, hipMemcpyDeviceToHost));
     (void)hipFree(d_img);
     (void)hipFree(d_pbo);
+    return PT_OK;
+}
+
+int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset) {
+    RC(need_init());
+    if (!out || n < 0 || n > 16) return fail(PT_E_INVALID, "bad arguments");
+    HIPCHK(hipStreamSynchronize(g.stream));
+    unsigned long long tmp[16];
+    HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) out[i] = tmp[i];
+    if (reset) {
+        memset(tmp, 0, sizeof tmp);
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_sections), tmp, sizeof tmp, 0, hipMemcpyHostToDevice));
+    }
     return PT_OK;
 }
 

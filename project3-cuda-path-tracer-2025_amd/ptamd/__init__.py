@@ -90,6 +90,7 @@ ABI_SYMBOLS = [
     "pt_trace", "pt_trace_frames", "pt_synchronize", "pt_get_image", "pt_get_image_device", "pt_set_image",
     "pt_get_frame_stats", "pt_reset_stats", "pt_set_camera", "pt_scene_load", "pt_scene_get_view", "pt_scene_get_info",
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
+    "pt_debug_section_counters",
     "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames",
 ]
 
@@ -115,6 +116,7 @@ def _load():
         "pt_test_shade": (i32, [i32, vp, vp, i64]), "pt_test_compact": (i32, [vp, i64, vp, vp]),
         "pt_test_sort": (i32, [vp, i64, vp]), "pt_test_rng": (i32, [vp, i64, i32, vp]),
         "pt_test_pbo": (i32, [vp, i64, i32, vp]), "pt_profile_frames": (i32, [i32, i32, vp]),
+        "pt_debug_section_counters": (i32, [vp, i32, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -298,6 +300,15 @@ class PathTracer:
                 "bounce_ms": [t.bounce_ms[i] for i in range(max(1, self.trace_depth))],
                 "compact_ms": t.compact_ms, "intersect_ms": t.intersect_ms, "shade_ms": t.shade_ms,
                 "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms}
+
+    SECTIONS = ["load", "cull", "exact", "finish", "shade", "store", "n_exact", "n_cand", "n_iters", "n_waves",
+                "n_lanes"]
+
+    def section_counters(self, reset: bool = True) -> dict:
+        """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""
+        buf = (ctypes.c_uint64 * 16)()
+        _check(lib.pt_debug_section_counters(buf, 16, int(reset)), "pt_debug_section_counters")
+        return {k: int(buf[i]) for i, k in enumerate(self.SECTIONS)}
 
     # ---- single-kernel entry points (tests) ----
     def test_camera(self, iteration: int) -> np.ndarray:

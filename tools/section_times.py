@@ -1,0 +1,48 @@
+"""Where the fused bounce kernel spends its cycles: runs the section-timing variant
+(pt_options.variant bit 4, wave-level s_memtime deltas) and prints per-section shares and work
+counters per live lane.
+
+    python tools/section_times.py [--scene cornell] [--frames 16] [--variant 6]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "project3-cuda-path-tracer-2025_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--variant", type=int, default=6)
+    ap.add_argument("--res", default="")
+    args = ap.parse_args()
+    import ptamd
+    res = tuple(int(x) for x in args.res.split("x")) if args.res else None
+    sc = ptamd.SceneFile(os.path.join(REPO, "scenes", args.scene + ".json"), res=res)
+    tr = ptamd.PathTracer(sc, variant=args.variant)
+    tr.trace_frames(1, 8)
+    tr.synchronize()
+    tr.section_counters(reset=True)
+    tr.trace_frames(9, args.frames)
+    tr.synchronize()
+    c = tr.section_counters(reset=True)
+    secs = ["load", "cull", "exact", "finish", "shade", "store"]
+    tot = sum(c[k] for k in secs)
+    lanes = max(1, c["n_lanes"])
+    out = {"scene": args.scene, "frames": args.frames,
+           "cycle_share": {k: round(c[k] / tot, 4) for k in secs},
+           "wave_cycles_per_wave": {k: round(c[k] / max(1, c["n_waves"]), 1) for k in secs},
+           "exact_tests_per_live_lane": round(c["n_exact"] / lanes, 3),
+           "candidates_per_live_lane": round(c["n_cand"] / lanes, 3),
+           "loop_iters_per_wave": round(c["n_iters"] / max(1, c["n_waves"]), 3),
+           "live_lanes_per_wave": round(lanes / max(1, c["n_waves"]), 2), "raw": c}
+    print(json.dumps(out, indent=1))
+    tr.free()
+
+
+if __name__ == "__main__":
+    main()
