@@ -6,18 +6,20 @@
  *
  * Parity status (details in DESIGN.md "Oracle"):
  *   - RNG (utilhash + thrust::default_random_engine + uniform_real_distribution<float>):
- *     pinned bit-exactly against rocThrust 2.8.5 (THRUST_VERSION 200805, the reference's
- *     third-party dependency) by oracle/ref_pins/rng_pin.cpp -> tests/golden/rng_pin.json.
- *   - glm 0.9.6 semantics (TRS matrices, inverse, inverseTranspose, normalize/reflect/refract):
- *     pinned bit-exactly against the reference's vendored glm headers and its own
- *     src/utilities.cpp compiled from source (oracle/ref_pins/glm_pin.cpp).
- *   - scene ingest order (alphabetical material ids): pinned against the vendored
- *     nlohmann json 3.11.3 (oracle/ref_pins/json_pin.cpp).
+ *     pinned bit-exactly against rocThrust (THRUST_VERSION 200805, the implementation in this
+ *     image of the reference's third-party Thrust dependency) by oracle/ref_pins/rng_pin.cpp ->
+ *     tests/golden/rng_pin.json.
+ *   - glm 0.9.6 semantics (TRS matrices, inverse, inverseTranspose, normalize/reflect/refract),
+ *     the camera set-up float order and the alphabetical material ids: pinned bit-exactly
+ *     against the reference's own src/utilities.cpp, its vendored glm 0.9.6 and nlohmann json
+ *     3.11.3, compiled from /root/reference by oracle/ref_pins/ingest_pin.cpp ->
+ *     tests/golden/ingest_pin.json.
  *   - the device functions of src/intersections.cu, src/interactions.cu, src/pathtrace.cu:
  *     the reference's path needs the CUDA toolkit (cuda_runtime.h, thrust) which this image
  *     lacks, so it is UNBUILDABLE here; their restatement is pinned only by the known answers
- *     SURVEY.md §8a records from a run of the reference (per-bounce live-path counts, first NaN
- *     pixel) -> tests/test_oracle_known_answers.py.  Beyond those: parity unpinned.
+ *     SURVEY.md §8a records from a run of the reference (cornell 800x800 per-bounce live-path
+ *     counts, glass-scene segment total, first NaN pixel) -> tests/test_oracle_pins.py.
+ *     Beyond those: parity unpinned.
  *
  * Layouts are the reference's own (include/pt/scene_structs.h): AoS PathSegment /
  * ShadeableIntersection, exactly as pathtrace.cu holds them.

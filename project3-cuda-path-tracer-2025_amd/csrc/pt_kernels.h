@@ -24,7 +24,7 @@ enum : int {
     VAR_WAVE_ATOMIC = 1,   // compaction: one atomic per wave, no block barrier
     VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
     VAR_SECTION_TIMING = 4,
-    VAR_OCC8 = 8,          // fused kernel compiled for 8 waves/SIMD (<= 64 VGPRs)// tools only: per-wave shader-clock section times into g_sections
+    VAR_CTILE8 = 16,       // staged compaction: 8 items per thread (2048-item tiles)// tools only: per-wave shader-clock section times into g_sections
 };
 
 struct CamDev {

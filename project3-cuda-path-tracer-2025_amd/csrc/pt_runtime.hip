@@ -111,7 +111,7 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
 // FUSED: camera (bounce 0) | load -> intersect -> shade -> gather dead -> compact survivors
 // --------------------------------------------------------------------------------------------
 template <bool FIRST, bool HAS_BVH, int VAR>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu((VAR & VAR_OCC8) ? 8 : 1))) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride) {
     // dynamic LDS: [geom table, sc.num_geoms <= LDS_GEOMS, candidate-queue variants]
     //              [HAS_BVH: traversal stack, stack_depth x BLOCK ints]
@@ -275,13 +275,15 @@ __global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBu
 //   k_compact_scan    one workgroup: exclusive scan of tile_cnt -> tile_off, total -> n_out
 //   k_compact_scatter per tile: flags + survivor payload loaded together, wave ballot/mbcnt
 //                     ranks in item order, stores to tile_off[t] + rank (stable)
-constexpr int CITEMS = 4;                       // items per thread
-constexpr int CTILE = BLOCK * CITEMS;           // 1024 items per tile
+constexpr int CITEMS = 4;                       // items per thread (8 spills: measured slower)
+constexpr int CTILE_MIN = BLOCK * CITEMS;       // 1024-item tiles (sizes the tile arrays)
 constexpr int STILE = BLOCK * 8;                // material-sort tile (2048 items)
 constexpr int SCAN_THREADS = 1024;
 
+template <int CITEMS>
 __global__ __launch_bounds__(BLOCK) void k_compact_count(const int* __restrict__ alive, const int* n_ptr,
                                                          int* __restrict__ tile_cnt) {
+    constexpr int CTILE = BLOCK * CITEMS;
     __shared__ int s_w[BLOCK / 64];
     const int n = *n_ptr;
     const int base = blockIdx.x * CTILE;
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(BLOCK) void k_compact_count(const int* __restrict__
 }
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_compact_scan(const int* __restrict__ tile_cnt, const int* n_ptr,
-                                                                int* __restrict__ tile_off, int* n_out) {
+                                                                int* __restrict__ tile_off, int* n_out, int CTILE) {
     __shared__ int s_part[SCAN_THREADS];
     const int n = *n_ptr;
     const int ntiles = (n + CTILE - 1) / CTILE;
@@ -329,30 +331,36 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_compact_scan(const int* __rest
     if (tid == SCAN_THREADS - 1) *n_out = s_part[SCAN_THREADS - 1];
 }
 
+// native 4-float vector: arrays of it stay in VGPRs (HIP's float4 is a union wrapper, and
+// arrays of it were demoted to LDS/scratch, serialising each item's loads behind a wait)
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <int CITEMS>
 __global__ __launch_bounds__(BLOCK) void k_compact_scatter(const float4* __restrict__ inA, const float4* __restrict__ inB,
                                                            const float4* __restrict__ inC, float4* __restrict__ outA,
                                                            float4* __restrict__ outB, float4* __restrict__ outC,
                                                            const int* __restrict__ alive, const int* n_ptr,
                                                            const int* __restrict__ tile_off) {
+    constexpr int CTILE = BLOCK * CITEMS;
     __shared__ int s_cnt[CITEMS][BLOCK / 64];
     const int n = *n_ptr;
     const int base = blockIdx.x * CTILE;
     if (base >= n) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    int av[CITEMS];
-#pragma unroll
-    for (int k = 0; k < CITEMS; ++k) av[k] = alive[base + k * BLOCK + tid];
+    const v4f* iA = reinterpret_cast<const v4f*>(inA);
+    const v4f* iB = reinterpret_cast<const v4f*>(inB);
+    const v4f* iC = reinterpret_cast<const v4f*>(inC);
     bool f[CITEMS];
 #pragma unroll
-    for (int k = 0; k < CITEMS; ++k) f[k] = (base + k * BLOCK + tid < n) & (av[k] != 0);
-    float4 a[CITEMS], b[CITEMS], c[CITEMS];
+    for (int k = 0; k < CITEMS; ++k) f[k] = (base + k * BLOCK + tid < n) & (alive[base + k * BLOCK + tid] != 0);
+    v4f a[CITEMS], b[CITEMS], c[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
-        int idx = base + k * BLOCK + tid;
+        const int idx = base + k * BLOCK + tid;
         if (f[k]) {
-            a[k] = inA[idx];
-            b[k] = inB[idx];
-            c[k] = inC[idx];
+            a[k] = __builtin_nontemporal_load(iA + idx);
+            b[k] = __builtin_nontemporal_load(iB + idx);
+            c[k] = __builtin_nontemporal_load(iC + idx);
         }
     }
     uint64_t m[CITEMS];
@@ -363,23 +371,29 @@ __global__ __launch_bounds__(BLOCK) void k_compact_scatter(const float4* __restr
     }
     __syncthreads();
     // exclusive offsets in item order (k-major, then wave): every thread recomputes its own
-    int off[CITEMS];
     int run = tile_off[blockIdx.x];
+    int off[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
+        int mine = run;
 #pragma unroll
         for (int i = 0; i < BLOCK / 64; ++i) {
-            if (i == w) off[k] = run;
-            run += s_cnt[k][i];
+            const int cnt = s_cnt[k][i];
+            mine = (i < w) ? mine + cnt : mine;
+            run += cnt;
         }
+        off[k] = mine;
     }
+    v4f* oA = reinterpret_cast<v4f*>(outA);
+    v4f* oB = reinterpret_cast<v4f*>(outB);
+    v4f* oC = reinterpret_cast<v4f*>(outC);
 #pragma unroll
     for (int k = 0; k < CITEMS; ++k) {
         if (f[k]) {
-            int dst = off[k] + mbcnt(m[k]);
-            outA[dst] = a[k];
-            outB[dst] = b[k];
-            outC[dst] = c[k];
+            const int dst = off[k] + mbcnt(m[k]);
+            __builtin_nontemporal_store(a[k], oA + dst);
+            __builtin_nontemporal_store(b[k], oB + dst);
+            __builtin_nontemporal_store(c[k], oC + dst);
         }
     }
 }
@@ -627,8 +641,6 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 1: launch_bounce_t<FIRST, HAS_BVH, 1>(grid, in, out, b); break;
         case 2: launch_bounce_t<FIRST, HAS_BVH, 2>(grid, in, out, b); break;
         case 6: launch_bounce_t<FIRST, HAS_BVH, 6>(grid, in, out, b); break;
-        case 10: launch_bounce_t<FIRST, HAS_BVH, 10>(grid, in, out, b); break;
-        case 11: launch_bounce_t<FIRST, HAS_BVH, 11>(grid, in, out, b); break;
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -642,6 +654,18 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     }
 }
 
+// stable compaction of the n_in paths of `pi` into `po` (three launches, see k_compact_*)
+template <int CITEMS>
+void launch_compact(PathBuf pi, PathBuf po, const int* n_in, int* n_out, int npaths) {
+    constexpr int CTILE = BLOCK * CITEMS;
+    const int ntiles = (npaths + CTILE - 1) / CTILE;
+    launch(5, k_compact_count<CITEMS>, dim3(ntiles), dim3(BLOCK), 0, (const int*)g.d_alive, n_in, g.d_tile_cnt);
+    launch(5, k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, (const int*)g.d_tile_cnt, n_in, g.d_tile_off, n_out,
+           CTILE);
+    launch(3, k_compact_scatter<CITEMS>, dim3(ntiles), dim3(BLOCK), 0, (const float4*)pi.A, (const float4*)pi.B,
+           (const float4*)pi.C, po.A, po.B, po.C, (const int*)g.d_alive, n_in, (const int*)g.d_tile_off);
+}
+
 // Enqueue one pass's kernels (everything after k_frame_begin) on g.stream: `batch` frames
 // traced together as one wavefront of local_pixels x batch paths.
 int enqueue_pass_body(int batch) {
@@ -652,7 +676,7 @@ int enqueue_pass_body(int batch) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 15, dim3(nb), in, out, b);
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 7, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -661,7 +685,6 @@ int enqueue_pass_body(int batch) {
     // STAGED
     launch(0, k_camera, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(0), g.d_ctl);
     HIPCHK(hipGetLastError());
-    const int ntiles = (npaths + CTILE - 1) / CTILE;   // compaction tiles
     const int stiles = (npaths + STILE - 1) / STILE;   // material-sort tiles
     int cur = 0;
     for (int b = 0; b < nbounces; ++b) {
@@ -689,11 +712,7 @@ int enqueue_pass_body(int batch) {
         if (g.opts.stream_compaction) {
             PathBuf pi = pathbuf(cur), po = pathbuf(cur ^ 1);
             int* n_out = &g.d_ctl->cnt[b + 1][0][0];
-            launch(5, k_compact_count, dim3(ntiles), dim3(BLOCK), 0, (const int*)g.d_alive, n_in, g.d_tile_cnt);
-            launch(5, k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, (const int*)g.d_tile_cnt, n_in, g.d_tile_off,
-                   n_out);
-            launch(3, k_compact_scatter, dim3(ntiles), dim3(BLOCK), 0, (const float4*)pi.A, (const float4*)pi.B,
-                   (const float4*)pi.C, po.A, po.B, po.C, (const int*)g.d_alive, n_in, (const int*)g.d_tile_off);
+            launch_compact<CITEMS>(pi, po, n_in, n_out, npaths);
             HIPCHK(hipGetLastError());
             cur ^= 1;
         }
@@ -1099,7 +1118,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
     RC(dalloc(&g.d_alive, (size_t)g.capacity));
     RC(dalloc(&g.d_perm, (size_t)g.capacity));
-    const int ntiles = (g.capacity + CTILE - 1) / CTILE + 1;
+    const int ntiles = (g.capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
     RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, s->num_materials)));
     RC(dalloc(&g.d_tile_cnt, (size_t)ntiles));
     RC(dalloc(&g.d_tile_off, (size_t)ntiles));
@@ -1329,15 +1348,8 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     if (n) HIPCHK(hipMemcpy(g.d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
     RC(set_count(0, (int)n));
-    const int ntiles = (int)((n + CTILE - 1) / CTILE);
-    if (ntiles > 0) {
-        PathBuf pi = pathbuf(0), po = pathbuf(1);
-        hipLaunchKernelGGL(k_compact_count, dim3(ntiles), dim3(BLOCK), 0, g.stream, (const int*)g.d_alive,
-                           staged_count(0), g.d_tile_cnt);
-        hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, g.stream, (const int*)g.d_tile_cnt,
-                           staged_count(0), g.d_tile_off, &g.d_ctl->cnt[1][0][0]);
-        hipLaunchKernelGGL(k_compact_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, pi.A, pi.B, pi.C, po.A, po.B,
-                           po.C, (const int*)g.d_alive, staged_count(0), (const int*)g.d_tile_off);
+    if (n > 0) {   // the pipeline's launch sequence
+        launch_compact<CITEMS>(pathbuf(0), pathbuf(1), staged_count(0), &g.d_ctl->cnt[1][0][0], (int)n);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(g.stream));

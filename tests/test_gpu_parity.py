@@ -199,6 +199,7 @@ PASS_CASES = [
     ("cornell", (64, 64), None, {}, 2),
     ("cornell", (64, 64), None, {}, 4),
     ("cornell", (64, 64), None, {"pipeline": 1}, 3),
+    ("cornell", (96, 96), None, {"pipeline": 1}, 5),
     ("cornell", (64, 64), None, {"pipeline": 1, "stream_compaction": 0}, 4),
     ("cornell_glass_test", (64, 64), None, {"pipeline": 1, "material_sort": 1}, 2),
     ("cornell_glass_test", (48, 40), None, {"use_graph": 0}, 5),

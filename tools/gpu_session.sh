@@ -26,8 +26,12 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-        python bench.py --steps 30 --warmup 3 --no-cpu-baseline
+        python bench.py --steps 100 --warmup 10 --no-cpu-baseline
     step rocprof_staged 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_staged" -o run --output-format csv -- \
-        python bench.py --steps 30 --warmup 3 --no-cpu-baseline --pipeline staged
+        python bench.py --steps 100 --warmup 10 --no-cpu-baseline --pipeline staged
+fi
+if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
+    step pmc_fused 900 env PMC_TAG=fused_ bash tools/pmc.sh
+    step pmc_staged 900 env PMC_TAG=staged_ PMC_SETS="FETCH_SIZE;WRITE_SIZE" bash tools/pmc.sh --pipeline staged
 fi
 echo "session done"

@@ -7,14 +7,14 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p "$OUT"
 i=0
-SETS=${PMC_SETS:-"SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_VMEM;SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY;SQ_ACTIVE_INST_VALU,SQ_INST_CYCLES_VMEM,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum,TCC_MISS_sum"}
+SETS=${PMC_SETS:-"SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS;SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY;SQ_ACTIVE_INST_VALU,SQ_INSTS_VMEM,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum,TCC_MISS_sum"}
 IFS=';' read -ra SETARR <<< "$SETS"
 for set in "${SETARR[@]}"; do
     set=${set//,/ }
     i=$((i+1))
     echo "== pass $i: $set"
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d "$OUT/${PMC_TAG:-}p$i" -o run --output-format csv -- \
-        python bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" > "$OUT/${PMC_TAG:-}p$i.log" 2>&1
+        python bench.py --steps ${PMC_STEPS:-32} --warmup ${PMC_WARMUP:-8} --no-cpu-baseline "$@" > "$OUT/${PMC_TAG:-}p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ]; then tail -20 "$OUT/${PMC_TAG:-}p$i.log"; exit $rc; fi

@@ -1,7 +1,7 @@
 set -o pipefail
 timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/t.log 2>&1; tail -3 gpurun_out/t.log
 [ -n "${NO_SEC:-}" ] || timeout -k 10 300 python tools/section_times.py > gpurun_out/sec.log 2>&1 || exit 3
-timeout -k 10 300 python tools/ab_variants.py --variants ${AB_VARIANTS:-2} --fpp ${AB_FPP:-8} --rounds 3 > gpurun_out/ab0.log 2>&1 || exit 4
+timeout -k 10 300 python tools/ab_variants.py --variants ${AB_VARIANTS:-2} --fpp ${AB_FPP:-8} --rounds 3 --pipeline ${AB_PIPELINE:-0} > gpurun_out/ab0.log 2>&1 || exit 4
 python3 - <<'PY'
 import json
 import os
