@@ -154,10 +154,31 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             p = camera_ray(sc.cam, iter + slot, sc.trace_depth, shard_pixel(sc, gid - slot * sc.shard.local_pixels));
             p.slot = slot;
         } else {
-            int s = 0;
+            // input slot of live path gid: segment s holds [segoff[s], segoff[s+1]) at s*seg_stride.
+            // Resolved once per wave on the scalar unit; per lane only if the wave straddles a
+            // segment boundary (at most NSEG-1 waves per bounce).
+            const int w0 = block_start + (__builtin_amdgcn_readfirstlane(tid >> 6) << 6);
+            int lo = 0, hi = segoff[1], sb = 0;
 #pragma unroll
-            for (int k = 1; k < NSEG; ++k) s += (gid >= segoff[k]) ? 1 : 0;
-            p = load_path(in, s * seg_stride + (gid - segoff[s]));
+            for (int k = 1; k < NSEG; ++k)
+                if (w0 >= segoff[k]) {
+                    lo = segoff[k];
+                    hi = segoff[k + 1];
+                    sb = k;
+                }
+            int slot;
+            if (w0 + 63 < hi) {
+                slot = sb * seg_stride - lo + gid;
+            } else {
+                int sl = 0;
+#pragma unroll
+                for (int k = 1; k < NSEG; ++k) sl += (gid >= segoff[k]) ? 1 : 0;
+                int sofs = 0;
+#pragma unroll
+                for (int k = 1; k < NSEG; ++k) sofs = (sl == k) ? segoff[k] : sofs;
+                slot = sl * seg_stride + (gid - sofs);
+            }
+            p = load_path(in, slot);
         }
         if (TIMING) {
             __builtin_amdgcn_s_waitcnt(0);
