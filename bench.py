@@ -43,8 +43,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pipeline", choices=["fused", "staged"], default="fused")
     ap.add_argument("--scene", default=SCENE)
+    ap.add_argument("--sort", action="store_true", help="material sort (MATERIAL_SORTING, configs[2])")
+    ap.add_argument("--res", default="", help="WxH override (configs[4]: 1600x1600)")
+    ap.add_argument("--depth", type=int, default=-1, help="trace depth override (configs[4]: 12)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--shard", choices=["samples", "pixels"], default="samples",
+                    help="N>1: samples = every rank traces whole frames (weak scaling); pixels = each "
+                         "frame's interleaved row bands split over the ranks (strong scaling)")
     return ap.parse_args()
 
 
@@ -58,18 +64,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL (backend "nccl") in production; PT_BENCH_BACKEND=gloo rehearses the multi-rank logic
+    # with several ranks sharing one GPU (the framebuffer combine then goes through host memory)
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    device = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
-    scene = ptamd.SceneFile(args.scene)
+    res = tuple(int(x) for x in args.res.split("x")) if args.res else None
+    scene = ptamd.SceneFile(args.scene, res=res, depth=args.depth if args.depth >= 0 else None)
     pipeline = ptamd.PIPELINE_STAGED if args.pipeline == "staged" else ptamd.PIPELINE_FUSED
-    tr = ptamd.PathTracer(scene, device=local, pipeline=pipeline)
+    shard = {}
+    if world > 1 and args.shard == "pixels":
+        shard = dict(shard_mode=ptamd.SHARD_PIXELS, shard_rank=rank, shard_count=world, shard_rows=8)
+    tr = ptamd.PathTracer(scene, device=device, pipeline=pipeline, material_sort=int(args.sort), **shard)
     depth = scene.trace_depth
 
     # SAMPLES sharding: rank r traces the contiguous iteration block 1 + r*(W+K) .. (r+1)*(W+K)
-    # (ptamd.dist.sample_iterations), so its frames group into multi-frame passes
-    it = 1 + rank * (args.warmup + args.steps)
+    # (ptamd.dist.sample_iterations), so its frames group into multi-frame passes.  PIXELS: every
+    # rank traces iterations 1.. for its own row bands.
+    it = 1 + (rank * (args.warmup + args.steps) if not shard else 0)
     if args.warmup:
         tr.trace_frames(it, args.warmup)
         it += args.warmup
@@ -90,9 +108,12 @@ def main():
         prof = None
         tr.trace_frames(it, args.steps)
         tr.synchronize()
-        ptr, n = tr.image_device_ptr()
-        img = _device_tensor(torch, ptr, n, local, tr)
-        dist.reduce(img, dst=0, op=dist.ReduceOp.SUM)   # one RCCL framebuffer combine
+        if backend == "nccl":
+            ptr, n = tr.image_device_ptr()
+            img = _device_tensor(torch, ptr, n, device)
+        else:
+            img = torch.from_numpy(tr.image().reshape(-1))
+        dist.reduce(img, dst=0, op=dist.ReduceOp.SUM)   # one framebuffer combine (RCCL over xGMI)
         torch.cuda.synchronize()
     tr.synchronize()
     barrier()
@@ -103,7 +124,7 @@ def main():
     frames = st["frames_total"]
     assert frames == args.steps, (frames, args.steps)
     if world > 1:
-        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -112,8 +133,13 @@ def main():
     value = segs / elapsed / 1e6
 
     if rank == 0:
+        headline = (os.path.abspath(args.scene) == SCENE and not args.res and args.depth < 0 and not args.sort)
+        name = os.path.basename(args.scene)
+        workload = (f"{name} {tr.width}x{tr.height} depth {depth}, stream compaction on, "
+                    f"sort {'on' if args.sort else 'off'}")
         line = {
-            "metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8",
+            "metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8" if headline
+                      else f"Mpaths/s (rays x bounces / s), {workload}",
             "value": round(value, 2),
             "unit": "Mpaths/s",
             "n_gpus": world,
@@ -121,15 +147,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(REF_MS_PER_FRAME / ms_per_step, 2),
-            "vs_baseline_basis": "reference ms/frame 42.204 (README.md:136, RTX 3060 Laptop) / our ms_per_step",
+            "scaling": "strong" if shard else "weak",
+            "vs_baseline": round(REF_MS_PER_FRAME / ms_per_step, 2) if headline else None,
+            "vs_baseline_basis": "reference ms/frame 42.204 (README.md:136, RTX 3060 Laptop) / our ms_per_step"
+                                 if headline else "no published reference number for this workload",
             "dtype": "f32",
-            "data": "scenes/cornell.json from the reference (800x800, depth 8, 1 spp per step); no synthetic inputs",
-            "config": {"workload": "cornell.json 800x800 depth 8, stream compaction on, sort off (BASELINE configs[1])",
-                       "pipeline": args.pipeline, "segments_per_frame": round(segs / args.steps / world, 1),
+            "data": f"scenes/{name} from the reference ({tr.width}x{tr.height}, depth {depth}, 1 spp per step)"
+                    + ("; synthetic stand-in meshes (reference OBJs absent)" if "obj" in name else
+                       "; no synthetic inputs"),
+            "config": {"workload": workload + (" (BASELINE configs[1])" if headline else ""),
+                       "pipeline": args.pipeline, "segments_per_frame": round(segs / args.steps / (1 if shard else world), 1),
                        "frames_per_pass": st["frames_per_pass"],
-                       "parallelism": f"sample-sharded x{world}" if world > 1 else "single GPU"},
+                       "parallelism": (f"{args.shard}-sharded x{world}" if world > 1 else "single GPU")},
         }
         if prof is not None:
             line["roofline"] = roofline(prof, st, args, depth)
@@ -145,15 +174,11 @@ def main():
         dist.destroy_process_group()
 
 
-def _device_tensor(torch, ptr, n, device, tr):
+def _device_tensor(torch, ptr, n, device):
     """Zero-copy torch view of the library's image buffer (same HIP runtime)."""
     class _Cai:
         __cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 2}
-    try:
-        return torch.as_tensor(_Cai(), device=f"cuda:{device}")
-    except Exception:
-        t = torch.from_numpy(tr.image().reshape(-1)).to(f"cuda:{device}")
-        return t
+    return torch.as_tensor(_Cai(), device=f"cuda:{device}")
 
 
 def roofline(prof, st, args, depth):
