@@ -149,6 +149,10 @@ int32_t pt_scene_get_info(const pt_scene_file* scene, int32_t* iterations, int32
 int32_t pt_scene_material_name(const pt_scene_file* scene, int32_t id, char* buf, int32_t cap);
 void pt_scene_free(pt_scene_file* scene);
 const char* pt_scene_last_error(void);
+/* Scene::loadTexture's decode (scene.cpp:366-392, stbi_load(..., STBI_rgb_alpha)): PNG -> RGBA8.
+ * Writes width/height; copies w*h*4 bytes into rgba when cap is large enough (rgba may be
+ * NULL to query the size).  PT_E_INVALID + pt_scene_last_error() on a decode failure. */
+int32_t pt_texture_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgba, int64_t cap);
 
 /* ---- test entry points: run one production kernel on caller data (reference layouts) ---- */
 /* generateRayFromCamera for every pixel of this process's shard -> out[pixels] */

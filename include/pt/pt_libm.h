@@ -12,10 +12,12 @@
  *
  * Method: promote the float argument to double, Cody–Waite reduce by pi/2 with a 3-part
  * constant (fdlibm's pio2_1/2/3), evaluate fdlibm's __kernel_sin / __kernel_cos minimax
- * polynomials (public-domain coefficients), round once to float.  Every operation is a plain
- * IEEE double op; callers MUST compile with -ffp-contract=off so no FMA is formed on either
- * side.  Result error is < 0.5 ulp + 2^-40 relative, i.e. correctly rounded except in
- * vanishingly rare near-halfway cases — identically on both sides.
+ * polynomials (public-domain coefficients) in Horner form with EXPLICIT fused multiply-adds
+ * (fma is exactly specified by IEEE 754, so the host's fma() and gfx950's v_fma_f64 return the
+ * same bits), round once to float.  Every other operation is a plain IEEE double op; callers
+ * MUST compile with -ffp-contract=off so no further FMA is formed on either side.  Result
+ * error is < 0.5 ulp + 2^-40 relative, i.e. correctly rounded except in vanishingly rare
+ * near-halfway cases — identically on both sides.
  *
  * This is test/product shared *libm*, not part of the reference algorithm.
  */
@@ -27,6 +29,8 @@
 #else
 #define PT_LIBM_FN static inline
 #endif
+
+PT_LIBM_FN double pt_libm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 PT_LIBM_FN double pt_libm_floor(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -41,12 +45,12 @@ PT_LIBM_FN double pt_kernel_sin(double x) {
                  S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                  S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
     double z = x * x;
-    double p = S5 + z * S6;
-    p = S4 + z * p;
-    p = S3 + z * p;
-    p = S2 + z * p;
-    p = S1 + z * p;
-    return x + (x * z) * p;
+    double p = pt_libm_fma(z, S6, S5);
+    p = pt_libm_fma(z, p, S4);
+    p = pt_libm_fma(z, p, S3);
+    p = pt_libm_fma(z, p, S2);
+    p = pt_libm_fma(z, p, S1);
+    return pt_libm_fma(x * z, p, x);
 }
 
 PT_LIBM_FN double pt_kernel_cos(double x) {
@@ -54,12 +58,12 @@ PT_LIBM_FN double pt_kernel_cos(double x) {
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
     double z = x * x;
-    double p = C5 + z * C6;
-    p = C4 + z * p;
-    p = C3 + z * p;
-    p = C2 + z * p;
-    p = C1 + z * p;
-    return (1.0 - 0.5 * z) + (z * z) * p;
+    double p = pt_libm_fma(z, C6, C5);
+    p = pt_libm_fma(z, p, C4);
+    p = pt_libm_fma(z, p, C3);
+    p = pt_libm_fma(z, p, C2);
+    p = pt_libm_fma(z, p, C1);
+    return pt_libm_fma(z * z, p, pt_libm_fma(-0.5, z, 1.0));
 }
 
 /* sin and cos of a float, each rounded once to float. */
@@ -78,11 +82,11 @@ PT_LIBM_FN void pt_sincosf(float xf, float* s_out, float* c_out) {
     const double PIO2_2 = 6.07710050630396597660e-11;   /* next 33 bits */
     const double PIO2_3 = 2.02226624871116645580e-21;   /* next 33 bits */
     const double PIO2_3T = 8.47842766036889956997e-32;  /* tail */
-    double k = pt_libm_floor(x * INV_PIO2 + 0.5);
-    double r = x - k * PIO2_1;
-    r = r - k * PIO2_2;
-    r = r - k * PIO2_3;
-    r = r - k * PIO2_3T;
+    double k = pt_libm_floor(pt_libm_fma(x, INV_PIO2, 0.5));
+    double r = pt_libm_fma(-k, PIO2_1, x);    /* k < 2^30: each step exact up to the last rounding */
+    r = pt_libm_fma(-k, PIO2_2, r);
+    r = pt_libm_fma(-k, PIO2_3, r);
+    r = pt_libm_fma(-k, PIO2_3T, r);
     long long ki = (long long)k;
     int q = (int)(ki & 3);
     double s = pt_kernel_sin(r);

@@ -4,6 +4,7 @@
 // pt_* PODs of pt/scene_structs.h, aliased to the reference's names.
 #pragma once
 
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -57,6 +58,7 @@ public:
 
     // framework additions
     std::vector<std::string> materialNames;   // index = material id (alphabetical)
+    std::vector<std::vector<uint8_t>> texturePixels;   // RGBA8 storage behind textures[i].data
     pt_scene_view view() const;               // borrowed flat view for pt_init
 
 private:
@@ -64,6 +66,7 @@ private:
     void loadFromOBJ(const std::string& objName, int materialID, const pt_mat4& transformMatrix,
                      const pt_mat4& invTransposeMatrix);
     void buildBVH();
+    int loadTexture(const std::string& texturePath);
 };
 
 // The interactive viewer's camera recompute that every reference frame sees: main.cpp:359-380

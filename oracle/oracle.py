@@ -66,7 +66,14 @@ class OrScene(ctypes.Structure):
                 ("triangles", ctypes.c_void_p), ("num_triangles", ctypes.c_int32),
                 ("tri_indices", ctypes.c_void_p), ("num_tri_indices", ctypes.c_int32),
                 ("bvh_nodes", ctypes.c_void_p), ("num_bvh_nodes", ctypes.c_int32),
-                ("camera", CameraC), ("trace_depth", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+                ("camera", CameraC), ("trace_depth", ctypes.c_int32), ("num_textures", ctypes.c_int32),
+                ("textures", ctypes.c_void_p)]
+
+
+class TextureC(ctypes.Structure):
+    """pt_texture (include/pt/scene_structs.h) == the reference's Texture (sceneStructs.h:60-66)"""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("_pad", ctypes.c_int32), ("data", ctypes.c_void_p)]
 
 
 class OrOptions(ctypes.Structure):
@@ -150,6 +157,7 @@ class Scene:
     iterations: int
     image_name: str
     material_names: list = field(default_factory=list)
+    textures: list = field(default_factory=list)     # (h, w, 4) uint8 RGBA arrays
 
     @property
     def width(self):
@@ -172,12 +180,30 @@ class Scene:
         s.bvh_nodes, s.num_bvh_nodes = _p(self.bvh_nodes), len(self.bvh_nodes)
         ctypes.memmove(ctypes.addressof(s.camera), self.camera.ctypes.data, 92)
         s.trace_depth = self.trace_depth
-        self._keep = s
+        tex = (TextureC * max(1, len(self.textures)))()
+        for i, t in enumerate(self.textures):
+            tex[i].width, tex[i].height, tex[i].channels = t.shape[1], t.shape[0], 4
+            tex[i].data = t.ctypes.data
+        s.num_textures, s.textures = len(self.textures), ctypes.addressof(tex)
+        self._keep = (s, tex)
         return s
 
 
-def _material(p: dict) -> np.void:
-    """`Material newMaterial{}` then the TYPE switch of scene.cpp:53-105."""
+def _load_texture(path: str, textures: list) -> int:
+    """Scene::loadTexture (scene.cpp:366-392): stbi_load(..., STBI_rgb_alpha) -> RGBA8; -1 on
+    failure.  Decoded here with Pillow, independently of the framework's own PNG decoder."""
+    try:
+        from PIL import Image
+        with Image.open(path) as im:
+            rgba = np.ascontiguousarray(np.asarray(im.convert("RGBA"), np.uint8))
+    except Exception:
+        return -1
+    textures.append(rgba)
+    return len(textures) - 1
+
+
+def _material(p: dict, json_path: str = "", textures: list | None = None) -> np.void:
+    """`Material newMaterial{}` then the TYPE switch of scene.cpp:53-133."""
     m = np.zeros(1, MATERIAL)[0]
     m["roughness"] = -1.0
     m["metallic"] = -1.0
@@ -210,15 +236,18 @@ def _material(p: dict) -> np.void:
         m["metallic"] = p["METALLIC"]
         m["indexOfRefraction"] = p["IOR"]
         m["color"] = rgb
-    # TEXTURE / BUMP_MAP (scene.cpp:106-133): textures are not carried by the oracle; a
-    # material that names one keeps hasTexture and an invalid id, which the reference's
-    # sampleTexture maps to magenta (pathtrace.cu:505-512).
+    # TEXTURE / BUMP_MAP (scene.cpp:102-133): path relative to the JSON's directory
+    # (basePath + "/" + name); a failed load leaves id -1 with hasTexture / hasBumpMap set.
+    k = json_path.rfind("/")
+    base = (json_path[:k] if k >= 0 else json_path)
+    if base and not base.endswith("/"):
+        base += "/"
     if "TEXTURE" in p:
+        m["textureID"] = _load_texture(base + p["TEXTURE"], textures) if textures is not None else -1
         m["hasTexture"] = 1
-        m["textureID"] = -1
     if "BUMP_MAP" in p:
+        m["bumpID"] = _load_texture(base + p["BUMP_MAP"], textures) if textures is not None else -1
         m["hasBumpMap"] = 1
-        m["bumpID"] = -1
         m["bumpScale"] = p["BUMP_SCALE"]
     return m
 
@@ -281,8 +310,9 @@ def load_scene(path: str, res=None, depth=None, obj_dir: str | None = None) -> S
     mats = data["Materials"]
     names = sorted(mats.keys())                     # nlohmann::json objects are std::map
     materials = np.zeros(len(names), MATERIAL)
+    textures = []
     for i, n in enumerate(names):
-        materials[i] = _material(mats[n])
+        materials[i] = _material(mats[n], path, textures)
     ids = {n: i for i, n in enumerate(names)}
     geoms, tris = [], []
     base = os.path.dirname(path) if obj_dir is None else obj_dir
@@ -322,7 +352,7 @@ def load_scene(path: str, res=None, depth=None, obj_dir: str | None = None) -> S
     return Scene(geoms=np.concatenate(geoms) if geoms else np.zeros(0, GEOM), materials=materials,
                  triangles=triangles, tri_indices=idx, bvh_nodes=nodes, camera=camera,
                  trace_depth=int(tdepth), iterations=int(cam["ITERATIONS"]), image_name=str(cam["FILE"]),
-                 material_names=names)
+                 material_names=names, textures=textures)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -9,6 +9,7 @@
  */
 #include "pt_oracle.h"
 #include "pt/pt_libm.h"
+#include "pt/pt_texture.h"
 
 #include <float.h>
 #include <math.h>
@@ -630,16 +631,31 @@ void or_scatter(const or_options* o, pt_path_segment* path, pt_vec3 intersect, p
     scatter_rng(o, path, intersect, normal, m, &rng);
 }
 
-/* pathtrace.cu:521-621 kernShadeMaterialProper, one path (textures: none loaded, so a
- * hasTexture material takes sampleTexture's "bad id" magenta, pathtrace.cu:505-512;
- * bump mapping needs bumpID >= 0 which needs a loaded texture, so it is skipped). */
+/* pathtrace.cu:505-519 sampleTexture / sampleHeight: tex2D<float4>(texObjects[id], x, 1 - y)
+ * through the framework's definition of CUDA's linear/wrap fetch (include/pt/pt_texture.h) */
+static v3 sample_texture(const or_scene* s, int texID, v2 uv) {
+    if (texID < 0 || texID >= s->num_textures) return V3(1.0f, 0.0f, 1.0f);
+    const pt_texture* t = &s->textures[texID];
+    float c[4];
+    pt_tex2d((const uint32_t*)t->data, t->width, t->height, uv.x, 1.f - uv.y, c);
+    return V3(c[0], c[1], c[2]);
+}
+static float sample_height(const or_scene* s, int texID, v2 uv) {
+    if (texID < 0 || texID >= s->num_textures) return 0.0f;
+    const pt_texture* t = &s->textures[texID];
+    float c[4];
+    pt_tex2d((const uint32_t*)t->data, t->width, t->height, uv.x, 1.f - uv.y, c);
+    return c[0];
+}
+
+/* pathtrace.cu:521-621 kernShadeMaterialProper, one path */
 void or_shade(const or_scene* s, const or_options* o, int32_t iter, const pt_shadeable_isect* isect,
               pt_path_segment* ps) {
     if (ps->remainingBounces <= 0) return;
     if (isect->t > 0.0f) {
         pt_material material = s->materials[isect->materialId];
         v3 materialColor = material.color;
-        if (material.hasTexture) materialColor = V3(1.0f, 0.0f, 1.0f);
+        if (material.hasTexture) materialColor = sample_texture(s, material.textureID, isect->uv);
         material.color = materialColor;
         if (material.emittance > 0.0f) {
             ps->color = mul3(ps->color, muls3(materialColor, material.emittance));
@@ -647,7 +663,28 @@ void or_shade(const or_scene* s, const or_options* o, int32_t iter, const pt_sha
         } else {
             or_rng rng = rng_make(iter, ps->pixelIndex, ps->remainingBounces);
             v3 intersect = add3(ps->ray.origin, muls3(ps->ray.direction, isect->t));
-            v3 shadingNormal = isect->surfaceNormal;
+            v3 ng = isect->surfaceNormal;
+            v3 dpdu = isect->dpdu, dpdv = isect->dpdv;
+            v2 uv = isect->uv;
+            v3 shadingNormal = ng;
+            /* :579-607; bumpID < num_textures always holds for ids loadTexture returns */
+            if (material.hasBumpMap && material.bumpID >= 0 && material.bumpID < s->num_textures) {
+                int bumpTexID = material.bumpID;
+                int texWidth = s->textures[bumpTexID].width;
+                int texHeight = s->textures[bumpTexID].height;
+                float du = 1.0f / (float)texWidth;
+                float dv = 1.0f / (float)texHeight;
+                float h = sample_height(s, bumpTexID, uv);
+                float hU = sample_height(s, bumpTexID, V2(uv.x + du, uv.y));
+                float hV = sample_height(s, bumpTexID, V2(uv.x, uv.y + dv));
+                float dhdu = (hU - h) / du;
+                float dhdv = (hV - h) / dv;
+                float scale = material.bumpScale;
+                v3 dpdu_p = add3(dpdu, muls3(ng, scale * dhdu));     /* dpdu + scale * dhdu * ng */
+                v3 dpdv_p = add3(dpdv, muls3(ng, scale * dhdv));
+                shadingNormal = normalize3(cross3(dpdu_p, dpdv_p));
+                if (dot3(shadingNormal, ng) < 0.0f) shadingNormal = neg3(shadingNormal);
+            }
             scatter_rng(o, ps, intersect, shadingNormal, &material, &rng);
         }
     } else {

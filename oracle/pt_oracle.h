@@ -42,7 +42,8 @@ typedef struct {
     const pt_bvh_node* bvh_nodes;  int32_t num_bvh_nodes;
     pt_camera camera;
     int32_t trace_depth;
-    int32_t _pad;
+    int32_t num_textures;
+    const pt_texture* textures;    /* RGBA8 (stbi STBI_rgb_alpha) images, scene.cpp:366-392 */
 } or_scene;
 
 typedef struct {

@@ -104,7 +104,7 @@ struct DevGeom {
 };
 static_assert(sizeof(DevGeom) == 192, "DevGeom");
 
-// 48-byte material: only what shading reads (sceneStructs.h:36-57)
+// 64-byte material: only what shading reads (sceneStructs.h:36-57)
 struct DevMaterial {
     float color[3];
     float emittance;
@@ -112,9 +112,12 @@ struct DevMaterial {
     float ior;
     int32_t hasTexture;
     int32_t textureID;
-    int32_t _pad;
+    int32_t hasBumpMap;
+    int32_t bumpID;
+    float bumpScale;
+    int32_t _pad[2];
 };
-static_assert(sizeof(DevMaterial) == 48, "DevMaterial");
+static_assert(sizeof(DevMaterial) == 64, "DevMaterial");
 
 // 32-byte BVH node: (min.xyz, a) (max.xyz, b); internal: a = left, b = right (<0: none);
 // leaf (reference: triCount > 0 && start >= 0): a = start, b = -(triCount + 2)
@@ -186,7 +189,20 @@ PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normaliz
 // (tmin_n), or the sphere's object-space hit point.
 PT_DEV float geom_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
     const f3 qo = xform(g.inv, ro, 1.0f);
-    const f3 qd = normalize(xform(g.inv, rd, 0.0f));
+    const f3 u = xform(g.inv, rd, 0.0f);
+    const float uu = dot(u, u);
+    if (g.type == PT_CUBE) {
+        // Early out that cannot change the result: on an axis where the object-space origin is
+        // outside the slab and the direction points away (qo > .5, u > 0 or qo < -.5, u < 0),
+        // both slab distances below are negative (|0.5 - qo| >= 2^-24, |qd| <= 1), so tmax < 0
+        // and the reference's test reports a miss.  sign(qd) = sign(u) because qd = u * s with
+        // s = 1/sqrt(uu) > 0 finite (uu < inf; u == +-0 underflow still gives -inf distances).
+        const bool away = (qo.x > 0.5f && u.x > 0.0f) || (qo.x < -0.5f && u.x < 0.0f) ||
+                          (qo.y > 0.5f && u.y > 0.0f) || (qo.y < -0.5f && u.y < 0.0f) ||
+                          (qo.z > 0.5f && u.z > 0.0f) || (qo.z < -0.5f && u.z < 0.0f);
+        if (away && uu < __builtin_inff()) return -1.0f;
+    }
+    const f3 qd = u * (1.0f / __builtin_sqrtf(uu));      // normalize(u), func_geometric.inl:158
     bool hit;
     float tq;
     f3 s = mk(0.f, 0.f, 0.f);

@@ -9,6 +9,7 @@
 #pragma once
 
 #include "pt_device.h"
+#include "pt/pt_texture.h"
 
 namespace ptd {
 
@@ -51,6 +52,9 @@ struct SceneDev {
     CamDev cam;
     ShardDev shard;
     float* contrib;     // passes of F > 1 frames: [slot][pixel] float3 of each terminated path
+    const uint32_t* texels;   // all textures' RGBA8 texels, concatenated
+    const int4* texinfo;      // per texture: texel offset, width, height
+    int num_textures;
 };
 
 // frame control block (device memory); zeroed / advanced by k_frame_begin every frame
@@ -366,19 +370,85 @@ PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
     return finish_hit<HAS_BVH>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
 }
 
-// kernShadeMaterialProper for one live path (pathtrace.cu:521-621).  Textures: a material
-// that names one with no loaded texture gets sampleTexture's magenta (pathtrace.cu:505-512).
-PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter) {
+// surface attributes of the winner that shading reads only for textured / bump-mapped
+// materials (ShadeableIntersection.uv / dpdu / dpdv, pathtrace.cu:439-446): interpolated uv and
+// the triangle's tangents for a mesh hit (intersections.cu:207-214), zeros for a primitive
+struct HitAttr {
+    float u, v;
+    f3 dpdu, dpdv;
+};
+PT_DEV HitAttr hit_attr(const SceneDev& sc, const Hit& h) {
+    HitAttr a;
+    a.u = 0.0f;
+    a.v = 0.0f;
+    a.dpdu = mk(0.f, 0.f, 0.f);
+    a.dpdv = mk(0.f, 0.f, 0.f);
+    if (h.tri >= 0) {
+        const DevTriCold& c = sc.cold[h.tri];
+        const float w0 = 1.0f - h.u - h.v;
+        a.u = (w0 * c.uv0[0] + h.u * c.uv1[0]) + h.v * c.uv2[0];
+        a.v = (w0 * c.uv0[1] + h.u * c.uv1[1]) + h.v * c.uv2[1];
+        a.dpdu = mk(c.dpdu[0], c.dpdu[1], c.dpdu[2]);
+        a.dpdv = mk(c.dpdv[0], c.dpdv[1], c.dpdv[2]);
+    }
+    return a;
+}
+
+// tex2D<float4>(texObjects[id], x, y) (pathtrace.cu:505-519) on the framework's texel store
+PT_DEV void tex_fetch(const SceneDev& sc, int id, float x, float y, float out[4]) {
+    const int4 ti = sc.texinfo[id];
+    pt_tex2d(sc.texels + ti.x, ti.y, ti.z, x, y, out);
+}
+
+// kernShadeMaterialProper for one live path (pathtrace.cu:521-621), with sampleTexture
+// (magenta for an id that names no loaded texture, pathtrace.cu:505-512) and the bump-map
+// normal perturbation (pathtrace.cu:579-607).  `attr()` yields the winner's HitAttr; it is
+// only evaluated for textured / bump-mapped materials.
+template <class AttrFn>
+PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter, AttrFn attr) {
     if (h.t > 0.0f) {
         const DevMaterial m = sc.mats[h.mat];
-        f3 mcolor = m.hasTexture ? mk(1.0f, 0.0f, 1.0f) : mk(m.color[0], m.color[1], m.color[2]);
+        f3 mcolor = mk(m.color[0], m.color[1], m.color[2]);
+        HitAttr ha;
+        ha.u = ha.v = 0.0f;
+        ha.dpdu = ha.dpdv = mk(0.f, 0.f, 0.f);
+        if (m.hasTexture | m.hasBumpMap) ha = attr();
+        const float uvx = ha.u, uvy = ha.v;
+        if (m.hasTexture) {
+            if (m.textureID < 0 || m.textureID >= sc.num_textures) {
+                mcolor = mk(1.0f, 0.0f, 1.0f);
+            } else {
+                float c[4];
+                tex_fetch(sc, m.textureID, uvx, 1.f - uvy, c);
+                mcolor = mk(c[0], c[1], c[2]);
+            }
+        }
         if (m.emittance > 0.0f) {
             p.c = p.c * (mcolor * m.emittance);
             p.rb = 0;
         } else {
             Rng rng = rng_make(iter, p.pix, p.rb);
             f3 intersect = p.o + p.d * h.t;
-            scatter(p, intersect, h.n, m, mcolor, rng, sc.arg_order);
+            f3 shadingNormal = h.n;
+            if (m.hasBumpMap && m.bumpID >= 0 && m.bumpID < sc.num_textures) {
+                const f3 ng = h.n;
+                const f3 dpdu = ha.dpdu, dpdv = ha.dpdv;
+                const int4 ti = sc.texinfo[m.bumpID];
+                const float du = 1.0f / float(ti.y);
+                const float dv = 1.0f / float(ti.z);
+                float t0[4], tu[4], tv[4];
+                tex_fetch(sc, m.bumpID, uvx, 1.f - uvy, t0);             // sampleHeight(.., uv)
+                tex_fetch(sc, m.bumpID, uvx + du, 1.f - uvy, tu);        // (uv.x + du, uv.y)
+                tex_fetch(sc, m.bumpID, uvx, 1.f - (uvy + dv), tv);      // (uv.x, uv.y + dv)
+                const float dhdu = (tu[0] - t0[0]) / du;
+                const float dhdv = (tv[0] - t0[0]) / dv;
+                const float scale = m.bumpScale;
+                const f3 dpdu_p = dpdu + ng * (scale * dhdu);
+                const f3 dpdv_p = dpdv + ng * (scale * dhdv);
+                shadingNormal = normalize(cross(dpdu_p, dpdv_p));
+                if (dot(shadingNormal, ng) < 0.0f) shadingNormal = -shadingNormal;
+            }
+            scatter(p, intersect, shadingNormal, m, mcolor, rng, sc.arg_order);
         }
     } else {
         p.c = mk(0.0f, 0.0f, 0.0f);

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             Hit h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING>(sc, s_geoms, p.o, p.d, s_stack + tid)
                               : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
             uint64_t ts = TIMING ? sec_clock() : 0;
-            shade_path(sc, p, h, iter + p.slot);
+            shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
             if (TIMING) {
                 tc = sec_clock();
                 sec_add(SEC_SHADE, tc - ts);
@@ -237,6 +237,8 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
 struct HitBuf {
     float4* nt;     // surfaceNormal.xyz | t
     int* mat;       // materialId
+    float4* uvd0;   // textured scenes only (else null): uv.xy | dpdu.xy
+    float4* uvd1;   //                                    dpdu.z | dpdv.xyz
 };
 
 __global__ __launch_bounds__(BLOCK) void k_camera(SceneDev sc, PathBuf out, FrameCtl* ctl) {
@@ -258,6 +260,11 @@ __global__ __launch_bounds__(BLOCK) void k_intersect(SceneDev sc, PathBuf in, Hi
     Hit h = intersect_scene<HAS_BVH>(sc, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), s_stack + threadIdx.x);
     hits.nt[gid] = make_float4(h.n.x, h.n.y, h.n.z, h.t);
     hits.mat[gid] = h.mat;
+    if (hits.uvd0) {
+        const HitAttr a = hit_attr(sc, h);
+        hits.uvd0[gid] = make_float4(a.u, a.v, a.dpdu.x, a.dpdu.y);
+        hits.uvd1[gid] = make_float4(a.dpdu.z, a.dpdv.x, a.dpdv.y, a.dpdv.z);
+    }
 }
 
 // shade (optionally through a material-sorted permutation); terminated paths are gathered
@@ -282,7 +289,19 @@ __global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBu
     h.tri = -1;
     h.u = h.v = 0.f;
     const int iter = iter_override > 0 ? iter_override : ctl->iter;
-    shade_path(sc, p, h, iter + p.slot);
+    shade_path(sc, p, h, iter + p.slot, [&]() {
+        HitAttr a;
+        a.u = a.v = 0.0f;
+        a.dpdu = a.dpdv = mk(0.f, 0.f, 0.f);
+        if (hits.uvd0) {
+            const float4 x = hits.uvd0[i], y = hits.uvd1[i];
+            a.u = x.x;
+            a.v = x.y;
+            a.dpdu = mk(x.z, x.w, y.x);
+            a.dpdv = mk(y.y, y.z, y.w);
+        }
+        return a;
+    });
     store_path(buf, i, p);
     if (p.rb <= 0 && image) gather_into_image(image, sc, iter_override > 0 ? 1 : ctl->batch, p);
     if (alive) alive[i] = p.rb > 0;
@@ -592,6 +611,10 @@ struct State {
     float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     float4* d_hit_nt = nullptr;
     int* d_hit_mat = nullptr;
+    float4* d_hit_uvd0 = nullptr;    // textured scenes only
+    float4* d_hit_uvd1 = nullptr;
+    uint32_t* d_texels = nullptr;
+    int4* d_texinfo = nullptr;
     int* d_alive = nullptr;
     int* d_perm = nullptr;
     int* d_tile_hist = nullptr;
@@ -711,7 +734,7 @@ int enqueue_pass_body(int batch) {
     for (int b = 0; b < nbounces; ++b) {
         // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
         const int* n_in = g.opts.stream_compaction ? staged_count(b) : staged_count(0);
-        HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+        HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
         if (g.has_bvh)
             launch(1, k_intersect<true>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
         else
@@ -804,7 +827,7 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_alive,
+    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
                     g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1061,6 +1084,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         d.ior = m.indexOfRefraction;
         d.hasTexture = m.hasTexture ? 1 : 0;
         d.textureID = m.textureID;
+        d.hasBumpMap = m.hasBumpMap ? 1 : 0;
+        d.bumpID = m.bumpID;
+        d.bumpScale = m.bumpScale;
     }
     // BVH: only when the reference would traverse it (BVH_ACCELERATION and a non-empty tree)
     g.has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
@@ -1137,6 +1163,30 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
     RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
     RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
+    // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
+    int num_tex = 0;
+    if (s->num_textures > 0 && s->textures) {
+        std::vector<int4> info(s->num_textures);
+        size_t total = 0;
+        for (int i = 0; i < s->num_textures; ++i) {
+            const pt_texture& t = s->textures[i];
+            if (t.width <= 0 || t.height <= 0 || !t.data || t.channels != 4)
+                return fail(PT_E_INVALID, "texture %d: need RGBA8 data (channels 4)", i);
+            info[i] = make_int4((int)total, t.width, t.height, 0);
+            total += (size_t)t.width * t.height;
+        }
+        if (total > (size_t)INT32_MAX) return fail(PT_E_UNSUPPORTED, "texture data too large");
+        RC(dalloc(&g.d_texels, total));
+        RC(dalloc(&g.d_texinfo, info.size()));
+        for (int i = 0; i < s->num_textures; ++i) {
+            const pt_texture& t = s->textures[i];
+            HIPCHK(hipMemcpy(g.d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
+        }
+        RC(upload(g.d_texinfo, info.data(), info.size()));
+        RC(dalloc(&g.d_hit_uvd0, (size_t)g.capacity));
+        RC(dalloc(&g.d_hit_uvd1, (size_t)g.capacity));
+        num_tex = s->num_textures;
+    }
     RC(dalloc(&g.d_alive, (size_t)g.capacity));
     RC(dalloc(&g.d_perm, (size_t)g.capacity));
     const int ntiles = (g.capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
@@ -1168,6 +1218,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
     sc.contrib = g.d_contrib;
+    sc.texels = g.d_texels;
+    sc.texinfo = g.d_texinfo;
+    sc.num_textures = num_tex;
     g.inited = true;
     HIPCHK(hipDeviceSynchronize());
     return PT_OK;
@@ -1307,7 +1360,7 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
     RC(set_count(0, (int)n));
-    HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+    HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
     if (g.has_bvh)
         hipLaunchKernelGGL((k_intersect<true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
                            pathbuf(0), hits, staged_count(0));
@@ -1320,11 +1373,23 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     std::vector<int> mat(n);
     HIPCHK(hipMemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
+    std::vector<float4> a0, a1;
+    if (g.d_hit_uvd0) {
+        a0.resize(n);
+        a1.resize(n);
+        HIPCHK(hipMemcpy(a0.data(), g.d_hit_uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(a1.data(), g.d_hit_uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
+    }
     for (int64_t i = 0; i < n; ++i) {
         memset(&isects[i], 0, sizeof(pt_shadeable_isect));
         isects[i].t = nt[i].w;
         isects[i].surfaceNormal = pt_vec3{nt[i].x, nt[i].y, nt[i].z};
         isects[i].materialId = mat[i];
+        if (g.d_hit_uvd0 && nt[i].w > 0.0f) {   // textured scenes: uv / dpdu / dpdv as the reference writes them
+            isects[i].uv = pt_vec2{a0[i].x, a0[i].y};
+            isects[i].dpdu = pt_vec3{a0[i].z, a0[i].w, a1[i].x};
+            isects[i].dpdv = pt_vec3{a1[i].y, a1[i].z, a1[i].w};
+        }
     }
     release_graph();
     HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
@@ -1348,7 +1413,17 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
     }
     HIPCHK(hipMemcpy(g.d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    HitBuf hits{g.d_hit_nt, g.d_hit_mat};
+    if (g.d_hit_uvd0) {
+        std::vector<float4> a0(n), a1(n);
+        for (int64_t i = 0; i < n; ++i) {
+            const pt_shadeable_isect& x = isects[i];
+            a0[i] = make_float4(x.uv.x, x.uv.y, x.dpdu.x, x.dpdu.y);
+            a1[i] = make_float4(x.dpdu.z, x.dpdv.x, x.dpdv.y, x.dpdv.z);
+        }
+        HIPCHK(hipMemcpy(g.d_hit_uvd0, a0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(g.d_hit_uvd1, a1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    }
+    HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
     hipLaunchKernelGGL(k_shade, dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), hits,
                        (const int*)nullptr, staged_count(0), (const FrameCtl*)g.d_ctl, iteration, (float*)nullptr,
                        (int*)nullptr);

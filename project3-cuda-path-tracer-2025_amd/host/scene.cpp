@@ -16,6 +16,7 @@
 #include "hmath.h"
 #include "json_lite.h"
 #include "scene.h"
+#include "png_decode.h"
 
 using namespace pth;
 
@@ -357,6 +358,27 @@ Scene::Scene(std::string filename, int resx, int resy, int depth) {
 
 Scene::~Scene() = default;
 
+// loadTexture (scene.cpp:366-392): RGBA8 via the framework's PNG decoder (stbi_load with
+// STBI_rgb_alpha in the reference; every texture the reference's scenes name is a PNG).
+int Scene::loadTexture(const std::string& texturePath) {
+    int w = 0, h = 0;
+    std::vector<uint8_t> rgba;
+    std::string err;
+    if (!ptio::png_load_rgba(texturePath, w, h, rgba, err)) {
+        std::fprintf(stderr, "Failed to load texture image: %s (%s)\n", texturePath.c_str(), err.c_str());
+        return -1;
+    }
+    texturePixels.push_back(std::move(rgba));
+    Texture t{};
+    t.width = w;
+    t.height = h;
+    t.channels = 4;
+    t.data = texturePixels.back().data();
+    int id = (int)textures.size();
+    textures.push_back(t);
+    return id;
+}
+
 void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int depth) {
     ptj::Value data = ptj::parse(read_file(jsonName));
     const ptj::Value& materialsData = data["Materials"];
@@ -396,15 +418,20 @@ void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int de
             m.indexOfRefraction = p["IOR"].as_float();
             m.color = vec3_of(p["RGB"]);
         }
-        // TEXTURE / BUMP_MAP (scene.cpp:106-133): image decoding is the next row of the
-        // build plan; until then the load "fails" exactly like a missing file in the
-        // reference (loadTexture returns -1, hasTexture stays true -> magenta).
+        // TEXTURE / BUMP_MAP (scene.cpp:102-133): path relative to the JSON's directory; a
+        // texture that fails to load gets id -1 while hasTexture / hasBumpMap stay set.
+        auto tex_base = [&]() {
+            size_t lastSlashPos = jsonName.find_last_of("/\\");
+            std::string basePath = lastSlashPos == std::string::npos ? jsonName : jsonName.substr(0, lastSlashPos);
+            if (!basePath.empty() && basePath.back() != '/' && basePath.back() != '\\') basePath += "/";
+            return basePath;
+        };
         if (p.contains("TEXTURE")) {
-            m.textureID = -1;
+            m.textureID = loadTexture(tex_base() + p["TEXTURE"].as_string());
             m.hasTexture = 1;
         }
         if (p.contains("BUMP_MAP")) {
-            m.bumpID = -1;
+            m.bumpID = loadTexture(tex_base() + p["BUMP_MAP"].as_string());
             m.hasBumpMap = 1;
             m.bumpScale = p["BUMP_SCALE"].as_float();
         }

@@ -5,6 +5,7 @@
 #include <string>
 
 #include "scene.h"
+#include "png_decode.h"
 
 struct pt_scene_file {
     Scene* scene;
@@ -17,6 +18,21 @@ thread_local std::string g_scene_err;
 extern "C" {
 
 const char* pt_scene_last_error(void) { return g_scene_err.c_str(); }
+
+int32_t pt_texture_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgba, int64_t cap) {
+    if (!path || !width || !height) return PT_E_INVALID;
+    int w = 0, h = 0;
+    std::vector<uint8_t> px;
+    std::string err;
+    if (!ptio::png_load_rgba(path, w, h, px, err)) {
+        g_scene_err = err;
+        return PT_E_INVALID;
+    }
+    *width = w;
+    *height = h;
+    if (rgba && cap >= (int64_t)px.size()) std::memcpy(rgba, px.data(), px.size());
+    return PT_OK;
+}
 
 // res <= 0 / depth < 0 keep the file's values; viewer_camera != 0 applies main.cpp's camera
 // recompute (what every reference frame actually renders with)

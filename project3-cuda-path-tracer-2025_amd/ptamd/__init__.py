@@ -90,7 +90,7 @@ ABI_SYMBOLS = [
     "pt_trace", "pt_trace_frames", "pt_synchronize", "pt_get_image", "pt_get_image_device", "pt_set_image",
     "pt_get_frame_stats", "pt_reset_stats", "pt_set_camera", "pt_scene_load", "pt_scene_get_view", "pt_scene_get_info",
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
-    "pt_debug_section_counters",
+    "pt_debug_section_counters", "pt_texture_load",
     "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames",
 ]
 
@@ -117,6 +117,7 @@ def _load():
         "pt_test_sort": (i32, [vp, i64, vp]), "pt_test_rng": (i32, [vp, i64, i32, vp]),
         "pt_test_pbo": (i32, [vp, i64, i32, vp]), "pt_profile_frames": (i32, [i32, i32, vp]),
         "pt_debug_section_counters": (i32, [vp, i32, i32]),
+        "pt_texture_load": (i32, [ctypes.c_char_p, vp, vp, vp, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -147,6 +148,23 @@ def default_options(**kw) -> _Options:
     return o
 
 
+def load_texture(path: str) -> np.ndarray:
+    """PNG -> (h, w, 4) uint8 RGBA with the scene loader's decoder (stbi STBI_rgb_alpha rules)."""
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    rc = lib.pt_texture_load(path.encode(), ctypes.byref(w), ctypes.byref(h), None, 0)
+    if rc != PT_OK:
+        raise PtError(f"pt_texture_load: {lib.pt_scene_last_error().decode(errors='replace')}")
+    out = np.empty((h.value, w.value, 4), np.uint8)
+    _check(lib.pt_texture_load(path.encode(), ctypes.byref(w), ctypes.byref(h), out.ctypes.data, out.size),
+           "pt_texture_load")
+    return out
+
+
+class _TextureC(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("_pad", ctypes.c_int32), ("data", ctypes.c_void_p)]
+
+
 class SceneFile:
     """The reference's Scene (scene.h:6-28) loaded by the framework's C++ loader."""
 
@@ -171,6 +189,11 @@ class SceneFile:
         self.tri_indices = self._arr(v.tri_indices, v.num_tri_indices, np.dtype("<i4"))
         self.bvh_nodes = self._arr(v.bvh_nodes, v.num_bvh_nodes, BVHNODE)
         self.camera = np.frombuffer(bytes(v.camera), CAMERA).copy()
+        self.textures = []                       # (h, w, 4) uint8 RGBA, Scene::textures order
+        for i in range(v.num_textures):
+            t = _TextureC.from_address(v.textures + i * ctypes.sizeof(_TextureC))
+            px = np.frombuffer((ctypes.c_uint8 * (t.width * t.height * 4)).from_address(t.data), np.uint8)
+            self.textures.append(px.reshape(t.height, t.width, 4).copy())
         self.material_names = []
         buf = ctypes.create_string_buffer(256)
         for i in range(v.num_materials):

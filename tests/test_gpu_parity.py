@@ -86,7 +86,7 @@ def _oracle_isects(oracle, a, paths):
     return out
 
 
-@pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy", "cornell_obj_khaslana"])
+@pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy", "cornell_obj_khaslana", "synthetic_textured_bump"])
 def test_intersect_bitexact(name, oracle, ptamd):
     a, b = _oracle_pair(oracle, ptamd, name, (96, 96))      # wavefront capacity >= 9216 paths
     tr = ptamd.PathTracer(b)
@@ -95,14 +95,20 @@ def test_intersect_bitexact(name, oracle, ptamd):
     paths = np.concatenate([paths.astype(oracle.PATH), cam])
     gpu = tr.test_intersect(paths)
     ref = _oracle_isects(oracle, a, paths)
-    for f in ("t", "surfaceNormal", "materialId"):
+    fields = ("t", "surfaceNormal", "materialId")
+    if len(a.textures):                      # textured scenes also carry uv / dpdu / dpdv
+        hit = ref["t"] > 0
+        ref["uv"][~hit], ref["dpdu"][~hit], ref["dpdv"][~hit] = 0, 0, 0
+        fields += ("uv", "dpdu", "dpdv")
+    for f in fields:
         assert _eq(gpu[f], ref[f]), (name, f, np.where(gpu[f].view(np.uint32) != ref[f].view(np.uint32))[0][:10])
-    assert (gpu["t"] > 0).mean() > 0.5
+    assert (gpu["t"] > 0).mean() > 0.3
     tr.free()
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_glass_test", "cornell_microfacet_test",
-                                  "cornell_reflective_test", "cornell_transmissive_test", "cornell_obj_bnnuy"])
+                                  "cornell_reflective_test", "cornell_transmissive_test", "cornell_obj_bnnuy",
+                                  "synthetic_textured_bump", "cornell_obj_phatphuck_microfacet"])
 def test_shade_bitexact(name, oracle, ptamd):
     import ctypes
     a, b = _oracle_pair(oracle, ptamd, name, (80, 80))      # wavefront capacity >= 6400 paths
@@ -174,6 +180,11 @@ FRAME_CASES = [
     ("cornell_obj_khaslana", (48, 48), 12, {}),
     ("cornell", (40, 30), 0, {}),
     ("cornell", (40, 30), 1, {"pipeline": 1}),
+    ("synthetic_textured_bump", (64, 64), None, {}),
+    ("synthetic_textured_bump", (64, 64), None, {"pipeline": 1}),
+    ("synthetic_textured_bump", (48, 48), None, {"pipeline": 1, "material_sort": 1}),
+    ("cornell_obj_phatphuck_texture_test", (48, 48), None, {}),
+    ("cornell_obj_phatphuck_microfacet", (48, 48), None, {"pipeline": 1}),
 ]
 
 
@@ -207,6 +218,7 @@ PASS_CASES = [
     ("cornell_obj_khaslana", (32, 32), 12, {"pipeline": 1}, 16),
     ("cornell", (40, 30), 0, {}, 3),
     ("cornell_microfacet_test", (50, 50), None, {"shard_mode": 1, "shard_rank": 1, "shard_count": 2}, 4),
+    ("synthetic_textured_bump", (48, 48), None, {}, 4),
 ]
 
 

@@ -29,6 +29,26 @@ def test_loader_bit_identical_to_oracle(name, oracle, ptamd):
         x, y = getattr(a, field), getattr(b, field)
         assert x.tobytes() == y.tobytes(), (name, field)
     assert (a.trace_depth, a.iterations, a.image_name) == (b.trace_depth, b.iterations, b.image_name)
+    # textures: the framework's PNG decoder vs the oracle's (Pillow), same ids / order
+    assert len(a.textures) == len(b.textures), name
+    for ta, tb in zip(a.textures, b.textures):
+        assert ta.shape == tb.shape and ta.tobytes() == tb.tobytes(), name
+
+
+def test_textured_scenes_load_textures(ptamd):
+    """Ids as scene.cpp:102-133 assigns them: materials in (alphabetical) load order, each
+    TEXTURE before its BUMP_MAP; -1 (with hasTexture kept) on failure, which takes no id."""
+    b = ptamd.SceneFile(scene_path("synthetic_textured_bump"))
+    m = dict(zip(b.material_names, b.materials))
+    assert len(b.textures) == 3 and all(t.shape == (512, 512, 4) for t in b.textures)
+    assert (m["textured_box"]["hasTexture"], m["textured_box"]["textureID"]) == (1, 0)
+    assert (m["textured_bump"]["hasTexture"], m["textured_bump"]["textureID"]) == (1, 1)
+    assert (m["textured_bump"]["hasBumpMap"], m["textured_bump"]["bumpID"]) == (1, 2)
+    assert abs(float(m["textured_bump"]["bumpScale"]) - 0.3) < 1e-7
+    assert (m["textured_missing"]["hasTexture"], m["textured_missing"]["textureID"]) == (1, -1)
+    t = ptamd.SceneFile(scene_path("cornell_obj_phatphuck_texture_test"))
+    tm = dict(zip(t.material_names, t.materials))["wood_textured_phat_phuck"]
+    assert (tm["textureID"], tm["hasBumpMap"], tm["bumpID"]) == (0, 1, -1)   # wood_normal.png is absent
 
 
 @pytest.mark.parametrize("res,depth", [((64, 64), 8), ((400, 400), 4), ((100, 37), 3)])
@@ -44,6 +64,8 @@ def test_loader_matches_reference_glm(ptamd):
         pin = json.load(f)
     n = 0
     for name in LOADABLE:
+        if name not in pin["scenes"]:          # our own synthetic scenes have no reference pin
+            continue
         ref = pin["scenes"][name]
         b = ptamd.SceneFile(scene_path(name))
         with open(scene_path(name)) as f:
