@@ -72,8 +72,10 @@ typedef struct pt_options {
     int32_t shard_rows;          /* PIXELS mode: height of the interleaved row bands (default 8) */
     int32_t block_size;          /* threads per block of the per-path kernels (default 256) */
     int32_t variant;             /* fused-kernel variant bits (1: per-wave compaction atomics,
-                                    2: per-lane candidate queue for the geom tests); results are
-                                    bit-identical for every value */
+                                    2: per-lane candidate queue for the geom tests, 4: section
+                                    timing (tools), 8: exact geom tests redistributed over the
+                                    wave's lanes); results are bit-identical for every value.
+                                    Default 2|8 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..16;
                                     0 = auto: ~5.2M paths in flight).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in

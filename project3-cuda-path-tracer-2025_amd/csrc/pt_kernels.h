@@ -25,6 +25,7 @@ enum : int {
     VAR_WAVE_ATOMIC = 1,   // compaction: one atomic per wave, no block barrier
     VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
     VAR_SECTION_TIMING = 4,
+    VAR_WAVE_REDIST = 8,   // intersection: the wave's (ray, candidate) pairs spread over all 64 lanes
     VAR_CTILE8 = 16,       // staged compaction: 8 items per thread (2048-item tiles)// tools only: per-wave shader-clock section times into g_sections
 };
 
@@ -64,7 +65,6 @@ struct FrameCtl {
     int _pad[2];
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
-    int ticket[MAXB];                       // dynamic tile ids of the staged compaction kernel
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
 };
 
@@ -398,6 +398,97 @@ PT_DEV HitAttr hit_attr(const SceneDev& sc, const Hit& h) {
 PT_DEV void tex_fetch(const SceneDev& sc, int id, float x, float y, float out[4]) {
     const int4 ti = sc.texinfo[id];
     pt_tex2d(sc.texels + ti.x, ti.y, ti.z, x, y, out);
+}
+
+// computeIntersections for a whole wave at once (VAR_WAVE_REDIST): every lane culls its ray,
+// the (lane, candidate geom) pairs of all 64 lanes are listed in LDS in (lane, geom) order and
+// the exact tests are dealt out 64 at a time, so a wave runs ceil(pairs / 64) exact-test rounds
+// instead of max-over-lanes(candidates).  Each lane then scans its own pairs in geom order with
+// the reference's `t > 0 && t_min > t` rule, so the winner (first minimum) is unchanged.  Every
+// lane of the wave must call this (uniform control flow); `live` = the lane has a ray.
+constexpr int WCAP = 192;      // pairs per wave held in LDS; more -> per-lane queue fallback
+struct WaveLds {
+    float ro[3][64], rd[3][64];
+    float rt[WCAP], rs[3][WCAP];
+    uint16_t task[WCAP];
+};
+PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, WaveLds* W,
+                           float& t_min, int& win, f3& seed) {
+    const int lane = threadIdx.x & 63;
+    uint64_t cand = 0;
+    CullRay cr;
+    if (live) {
+        cr = cull_ray(ro, rd);
+#pragma unroll 4
+        for (int i = 0; i < sc.num_geoms; ++i)
+            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
+    }
+    const int cnt = __builtin_popcountll(cand);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    const int excl = incl - cnt;
+    t_min = FLT_MAX_;
+    win = -1;
+    seed = mk(0.f, 0.f, 0.f);
+    if (total > WCAP) {                          // rare: per-lane queue (same results)
+        while (__any(cand != 0)) {
+            if (cand != 0) {
+                const int i = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const DevGeom& g = lg[i];
+                if (!cull_geom(g, cr, t_min)) {
+                    f3 s;
+                    const float t = geom_test(g, ro, rd, s);
+                    if (t > 0.0f && t_min > t) {
+                        t_min = t;
+                        win = i;
+                        seed = s;
+                    }
+                }
+            }
+        }
+        return;
+    }
+    W->ro[0][lane] = ro.x;
+    W->ro[1][lane] = ro.y;
+    W->ro[2][lane] = ro.z;
+    W->rd[0][lane] = rd.x;
+    W->rd[1][lane] = rd.y;
+    W->rd[2][lane] = rd.z;
+    {
+        int j = excl;
+        for (uint64_t m = cand; m; m &= m - 1) W->task[j++] = (uint16_t)((lane << 8) | __builtin_ctzll(m));
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int base = 0; base < total; base += 64) {
+        const int k = base + lane;
+        if (k < total) {
+            const int task = W->task[k];
+            const int src = task >> 8, gi = task & 255;
+            const f3 o = mk(W->ro[0][src], W->ro[1][src], W->ro[2][src]);
+            const f3 d = mk(W->rd[0][src], W->rd[1][src], W->rd[2][src]);
+            f3 s;
+            const float t = geom_test(lg[gi], o, d, s);
+            W->rt[k] = t;
+            W->rs[0][k] = s.x;
+            W->rs[1][k] = s.y;
+            W->rs[2][k] = s.z;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int j = excl; j < excl + cnt; ++j) {
+        const float t = W->rt[j];
+        if (t > 0.0f && t_min > t) {
+            t_min = t;
+            win = W->task[j] & 255;
+            seed = mk(W->rs[0][j], W->rs[1][j], W->rs[2][j]);
+        }
+    }
 }
 
 // kernShadeMaterialProper for one live path (pathtrace.cu:521-621), with sampleTexture

@@ -181,6 +181,10 @@ FRAME_CASES = [
     ("cornell", (40, 30), 0, {}),
     ("cornell", (40, 30), 1, {"pipeline": 1}),
     ("synthetic_textured_bump", (64, 64), None, {}),
+    ("cornell", (64, 64), None, {"variant": 10}),                       # wave-redistributed exact tests
+    ("cornell_glass_test", (64, 64), None, {"variant": 10}),
+    ("cornell_obj_bnnuy", (48, 48), None, {"variant": 10}),
+    ("synthetic_textured_bump", (48, 48), None, {"variant": 10}),
     ("synthetic_textured_bump", (64, 64), None, {"pipeline": 1}),
     ("synthetic_textured_bump", (48, 48), None, {"pipeline": 1, "material_sort": 1}),
     ("cornell_obj_phatphuck_texture_test", (48, 48), None, {}),
@@ -219,6 +223,7 @@ PASS_CASES = [
     ("cornell", (40, 30), 0, {}, 3),
     ("cornell_microfacet_test", (50, 50), None, {"shard_mode": 1, "shard_rank": 1, "shard_count": 2}, 4),
     ("synthetic_textured_bump", (48, 48), None, {}, 4),
+    ("cornell_multiple_glass", (64, 64), None, {"variant": 10}, 8),
 ]
 
 
