@@ -74,8 +74,9 @@ typedef struct pt_options {
     int32_t variant;             /* fused-kernel variant bits (1: per-wave compaction atomics,
                                     2: per-lane candidate queue for the geom tests, 4: section
                                     timing (tools), 8: exact geom tests redistributed over the
-                                    wave's lanes); results are bit-identical for every value.
-                                    Default 2|8 */
+                                    wave's lanes, 16: BVH traversal with exact-decision fast box
+                                    tests, near-first order and certified t-culling); results are
+                                    bit-identical for every value.  Default 2|8|16 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..16;
                                     0 = auto: ~5.2M paths in flight).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in

@@ -26,6 +26,7 @@ enum : int {
     VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
     VAR_SECTION_TIMING = 4,
     VAR_WAVE_REDIST = 8,   // intersection: the wave's (ray, candidate) pairs spread over all 64 lanes
+    VAR_BVH_FAST = 16,     // BVH: exact-decision fast AABB test, near-first order, certified t-culling
     VAR_CTILE8 = 16,       // staged compaction: 8 items per thread (2048-item tiles)// tools only: per-wave shader-clock section times into g_sections
 };
 
@@ -53,6 +54,7 @@ struct SceneDev {
     CamDev cam;
     ShardDev shard;
     float* contrib;     // passes of F > 1 frames: [slot][pixel] float3 of each terminated path
+    const float4* node_aux;   // per BVH node: MT error coefficient, max edge, reference DFS rank
     const uint32_t* texels;   // all textures' RGBA8 texels, concatenated
     const int4* texinfo;      // per texture: texel offset, width, height
     int num_textures;
@@ -71,7 +73,7 @@ struct FrameCtl {
 // VAR_SECTION_TIMING (tools/section_times.py): wave-level s_memtime deltas per kernel section and
 // per-lane work counters, summed by the first active lane of each wave
 enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
-       SEC_N_WAVES, SEC_N_LANES, SEC_COUNT };
+       SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_COUNT };
 __device__ unsigned long long g_sections[16];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
 PT_DEV void sec_add(int k, uint64_t v) {
@@ -81,10 +83,8 @@ PT_DEV void sec_add(int k, uint64_t v) {
     const int first = __builtin_ctzll(__builtin_amdgcn_read_exec());
     if (lane == first) atomicAdd(&g_sections[k], (unsigned long long)v);
 }
-PT_DEV void sec_add_lanes(int k, int v) {    // sum over the wave's active lanes
-    int s = v;
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    sec_add(k, (uint64_t)s);
+PT_DEV void sec_add_lanes(int k, int v) {    // sum over the active lanes (may be called divergently)
+    if (v) atomicAdd(&g_sections[k], (unsigned long long)v);
 }
 
 // a wavefront of paths: three float4 streams
@@ -160,7 +160,9 @@ struct Hit {
 // pop right first), same strict `t < t_hit` acceptance, so exact-t ties resolve identically.
 // `stack` is this thread's column of an LDS array (stride BLOCK).  Returns the winner's leaf
 // slot (index into the leaf-ordered hot triangle array) in `btri`.
+template <bool COUNT = false>
 PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& bu, float& bv, int& btri) {
+    int n_nodes = 0, n_tris = 0, n_it = 0;
     float t_hit = FLT_MAX_;
     bool hit = false;
     btri = -1;
@@ -170,10 +172,12 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
     while (sp > 0) {
         int ni = stack[(--sp) * BLOCK];
         DevNode nd = sc.nodes[ni];
+        if (COUNT) n_nodes++;
         if (!aabb_test(nd.lo, nd.hi, ro, rd)) continue;
         int a = __float_as_int(nd.lo.w), b = __float_as_int(nd.hi.w);
         if (b <= -2) {
             int cnt = -b - 2;
+            if (COUNT) n_tris += cnt;
             for (int i = 0; i < cnt; ++i) {
                 DevTriHot th = sc.hot[a + i];
                 f3 v0 = mk(th.a.x, th.a.y, th.a.z);
@@ -194,6 +198,140 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
             if (a >= 0 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = a;
             if (b >= 0 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = b;
         }
+    }
+    if (COUNT) {
+        sec_add_lanes(SEC_N_NODES, n_nodes);
+        sec_add_lanes(SEC_N_TRIS, n_tris);
+        sec_add_lanes(SEC_N_BVH_RAYS, 1);
+    }
+    return hit ? t_hit : -1.f;
+}
+
+// ---- faster traversal with the SAME result (VAR_BVH_FAST) ----------------------------------
+// 1. aabb_decide(): the reference's aabbIntersectionTest decision, computed with rcp slabs.
+//    Each slab distance differs from the reference's fl((b - o) / d) by < 2^-22 relative and
+//    has the same sign, so `t_max > 0` is decided exactly and `t_max >= t_min` whenever the gap
+//    exceeds 1e-6 (|t_min| + |t_max|); otherwise (or for a NaN ray) the reference arithmetic
+//    decides.  The visited node set is therefore the reference's.
+// 2. Children are visited nearest-entry first.  Ties in t are resolved by the reference's visit
+//    order (DFS rank of the leaf, then the slot), so the winner is the reference's: the first
+//    triangle of minimal t in ITS order.
+// 3. A node is skipped when its entry distance exceeds the best t so far (t_limit = the geoms'
+//    t_min included) by more than the Moller-Trumbore error bound of any triangle below it, so
+//    no skipped triangle could have tied or won.  For edges up to s and |det| >= 1e-5 (which
+//    intersectTriangle requires) with |d| = 1, the computed t of a hit differs from the
+//    geometric one by at most t * c (2 + s / t) (cross/dot rounding, relative) + c E (rounding
+//    of v1 - v0, v2 - v0, o - v0 for coordinates up to E, absolute), c = 64 * 2^-24 * s^2 / 1e-5
+//    (about 10x the first-order bound).  aux = (c, s, DFS rank, c E).
+PT_DEV bool aabb_decide(float4 lo, float4 hi, f3 ro, f3 rd, f3 rr, bool exact, float& entry) {
+    float tmin = -FLT_MAX_, tmax = FLT_MAX_;
+    const float bmin[3] = {lo.x, lo.y, lo.z};
+    const float bmax[3] = {hi.x, hi.y, hi.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float dir = comp(rd, i), origin = comp(ro, i);
+        if (__builtin_fabsf(dir) < 0.00001f) {
+            if (origin < bmin[i] || origin > bmax[i]) return false;
+        } else {
+            const float r = comp(rr, i);
+            const float t1 = (bmin[i] - origin) * r, t2 = (bmax[i] - origin) * r;
+            tmin = __builtin_fmaxf(tmin, __builtin_fminf(t1, t2));
+            tmax = __builtin_fminf(tmax, __builtin_fmaxf(t1, t2));
+        }
+    }
+    entry = tmin;
+    if (!exact) {
+        if (!(tmax > 0.f)) return false;
+        const float e = 1e-6f * (__builtin_fabsf(tmin) + __builtin_fabsf(tmax));
+        if (tmax - tmin > e) return true;
+        if (tmin - tmax > e) return false;
+    }
+    return aabb_test(lo, hi, ro, rd);
+}
+PT_DEV bool node_culled(float entry, float4 aux, float t_best) {
+    if (!(entry > 0.0f)) return false;
+    const float rho = aux.x * (2.0f + aux.y * __builtin_amdgcn_rcpf(t_best) * 1.001f) + 1e-6f;
+    return entry * (1.0f - 1e-6f) > t_best * (1.0f + rho) + aux.w;
+}
+// stack entry: node (16 bits) | entry distance truncated to bf16 (a lower bound for entry >= 0)
+PT_DEV uint32_t pack_entry(int node, float entry) {
+    const uint32_t eb = __float_as_uint(__builtin_fmaxf(entry, 0.0f)) >> 16;
+    return ((uint32_t)node << 16) | eb;
+}
+template <bool COUNT = false>
+PT_DEV float bvh_intersect_fast(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
+                                int& btri) {
+    int n_nodes = 0, n_tris = 0;
+    const bool exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
+                         rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);   // NaN / inf ray
+    const f3 rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    const bool packed = sc.num_nodes <= 65536;
+    float t_hit = FLT_MAX_;
+    bool hit = false;
+    int hit_rank = 0x7fffffff, hit_i = 0;
+    btri = -1;
+    float e0;
+    if (!aabb_decide(sc.nodes[0].lo, sc.nodes[0].hi, ro, rd, rr, exact, e0)) return -1.f;
+    int sp = 0;
+    stack[0] = packed ? (int)pack_entry(0, e0) : 0;
+    sp = 1;
+    while (sp > 0) {
+        const uint32_t w = (uint32_t)stack[(--sp) * BLOCK];
+        const int ni = packed ? (int)(w >> 16) : (int)w;
+        const float t_best = __builtin_fminf(t_hit, t_limit);
+        const float4 aux = sc.node_aux[ni];
+        if (packed && node_culled(__uint_as_float(w << 16), aux, t_best)) continue;
+        const DevNode nd = sc.nodes[ni];
+        const int a = __float_as_int(nd.lo.w), b = __float_as_int(nd.hi.w);
+        if (COUNT) n_nodes++;
+        if (b <= -2) {
+            const int cnt = -b - 2;
+            if (COUNT) n_tris += cnt;
+            const int rank = __float_as_int(aux.z);
+            for (int i = 0; i < cnt; ++i) {
+                const DevTriHot th = sc.hot[a + i];
+                const f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+                const f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+                const f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+                float t, u, v;
+                if (tri_test(ro, rd, v0, v1, v2, t, u, v) && t > 0.0f &&
+                    (t < t_hit || (t == t_hit && (rank < hit_rank || (rank == hit_rank && i < hit_i))))) {
+                    hit = true;
+                    t_hit = t;
+                    hit_rank = rank;
+                    hit_i = i;
+                    bu = u;
+                    bv = v;
+                    btri = a + i;
+                }
+            }
+        } else {
+            float ea = 0.f, eb = 0.f;
+            bool pa = a >= 0 && aabb_decide(sc.nodes[a].lo, sc.nodes[a].hi, ro, rd, rr, exact, ea);
+            bool pb = b >= 0 && aabb_decide(sc.nodes[b].lo, sc.nodes[b].hi, ro, rd, rr, exact, eb);
+            if (COUNT) {   // debug: the fast decision must equal the reference test
+                const bool ra = a >= 0 && aabb_test(sc.nodes[a].lo, sc.nodes[a].hi, ro, rd);
+                const bool rb = b >= 0 && aabb_test(sc.nodes[b].lo, sc.nodes[b].hi, ro, rd);
+                sec_add_lanes(SEC_N_BVH_ITERS, (ra != pa) + (rb != pb));
+            }
+            const float tb2 = __builtin_fminf(t_hit, t_limit);
+            if (pa && node_culled(ea, sc.node_aux[a], tb2)) pa = false;
+            if (pb && node_culled(eb, sc.node_aux[b], tb2)) pb = false;
+            // push the farther child first so the nearer one is popped first
+            int n1 = a, n2 = b;
+            float e1 = ea, e2 = eb;
+            bool p1 = pa, p2 = pb;
+            if (pa && pb && ea < eb) {
+                n1 = b; n2 = a; e1 = eb; e2 = ea;
+            }
+            if (p1 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = packed ? (int)pack_entry(n1, e1) : n1;
+            if (p2 && sp < sc.stack_depth) stack[(sp++) * BLOCK] = packed ? (int)pack_entry(n2, e2) : n2;
+        }
+    }
+    if (COUNT) {
+        sec_add_lanes(SEC_N_NODES, n_nodes);
+        sec_add_lanes(SEC_N_TRIS, n_tris);
+        sec_add_lanes(SEC_N_BVH_RAYS, 1);
     }
     return hit ? t_hit : -1.f;
 }
@@ -234,7 +372,7 @@ PT_DEV bool cull_geom(const DevGeom& g, const CullRay& c, float t_min) {
 
 // winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
 // miss / facing conventions of pathtrace.cu:397-446
-template <bool HAS_BVH>
+template <bool HAS_BVH, bool BVH_FAST = false, bool COUNT = false>
 PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
                       f3 seed) {
     Hit h;
@@ -254,7 +392,8 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
         if (sc.use_bvh && sc.num_nodes > 0) {
             float u, v;
             int tri;
-            float tb = bvh_intersect(sc, ro, rd, stack, u, v, tri);
+            float tb = BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
+                                : bvh_intersect<COUNT>(sc, ro, rd, stack, u, v, tri);
             if (tb > 0.0f && tb < t_min) {
                 t_min = tb;
                 hit_index = -2;
@@ -296,7 +435,7 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
 // computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
 // decides the winner (t and the normal "seed"); the world normal is derived once for the
 // winner — the same value the reference computes for every candidate and then keeps.
-template <bool HAS_BVH>
+template <bool HAS_BVH, bool BVH_FAST = false>
 PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
     float t_min = FLT_MAX_;
     int win = -1;
@@ -313,7 +452,7 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
             seed = s;
         }
     }
-    return finish_hit<HAS_BVH>(sc, sc.geoms, ro, rd, stack, t_min, win, seed);
+    return finish_hit<HAS_BVH, BVH_FAST>(sc, sc.geoms, ro, rd, stack, t_min, win, seed);
 }
 
 // computeIntersections with the exact per-geom tests driven by a per-lane candidate queue:
@@ -322,7 +461,7 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
 // and re-checks the cull against its current t_min before the exact test.  The wave executes
 // max-over-lanes(candidates) exact tests instead of one per geom any lane needs.
 // `lgeoms`: the block's LDS copy of the geom table (the caller's job; sc.num_geoms <= 64).
-template <bool HAS_BVH, bool TIMING = false>
+template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false>
 PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
     uint64_t tc0 = TIMING ? sec_clock() : 0;
     const CullRay cr = cull_ray(ro, rd);
@@ -363,11 +502,11 @@ PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
         sec_add(SEC_EXACT, tc2 - tc1);
         sec_add_lanes(SEC_N_EXACT, n_exact);
         sec_add(SEC_N_ITERS, (uint64_t)n_iters);
-        Hit h = finish_hit<HAS_BVH>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
+        Hit h = finish_hit<HAS_BVH, BVH_FAST, true>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
         sec_add(SEC_FINISH, sec_clock() - tc2);
         return h;
     }
-    return finish_hit<HAS_BVH>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
+    return finish_hit<HAS_BVH, BVH_FAST>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
 }
 
 // surface attributes of the winner that shading reads only for textured / bump-mapped

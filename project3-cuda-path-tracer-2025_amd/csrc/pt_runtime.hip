@@ -134,6 +134,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     constexpr bool TIMING = (VAR & VAR_SECTION_TIMING) != 0;
     constexpr bool QUEUE = (VAR & VAR_CAND_QUEUE) != 0;
     constexpr bool REDIST = (VAR & VAR_WAVE_REDIST) != 0;
+    constexpr bool BVH_FAST = (VAR & VAR_BVH_FAST) != 0;
     uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
     const bool lds_geoms = (QUEUE || REDIST) && sc.num_geoms <= LDS_GEOMS;
@@ -196,12 +197,12 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         int ww;
         f3 ws;
         wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, wt, ww, ws);
-        if (live) h = finish_hit<HAS_BVH>(sc, s_geoms, p.o, p.d, s_stack + tid, wt, ww, ws);
+        if (live) h = finish_hit<HAS_BVH, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid, wt, ww, ws);
     }
     if (live) {
         if (!(REDIST && lds_geoms))
-            h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING>(sc, s_geoms, p.o, p.d, s_stack + tid)
-                          : intersect_scene<HAS_BVH>(sc, p.o, p.d, s_stack + tid);
+            h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid)
+                          : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
         uint64_t ts = TIMING ? sec_clock() : 0;
         shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
         if (TIMING) {
@@ -261,14 +262,14 @@ __global__ __launch_bounds__(BLOCK) void k_camera(SceneDev sc, PathBuf out, Fram
     store_path(out, gid, p);
 }
 
-template <bool HAS_BVH>
+template <bool HAS_BVH, bool BVH_FAST>
 __global__ __launch_bounds__(BLOCK) void k_intersect(SceneDev sc, PathBuf in, HitBuf hits, const int* n_ptr) {
     extern __shared__ int s_stack[];
     const int n = *n_ptr;
     int gid = blockIdx.x * BLOCK + threadIdx.x;
     if (blockIdx.x * BLOCK >= n || gid >= n) return;
     float4 a = in.A[gid], b = in.B[gid];
-    Hit h = intersect_scene<HAS_BVH>(sc, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), s_stack + threadIdx.x);
+    Hit h = intersect_scene<HAS_BVH, BVH_FAST>(sc, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), s_stack + threadIdx.x);
     hits.nt[gid] = make_float4(h.n.x, h.n.y, h.n.z, h.t);
     hits.mat[gid] = h.mat;
     if (hits.uvd0) {
@@ -616,6 +617,7 @@ struct State {
     // device buffers
     DevGeom* d_geoms = nullptr;
     DevMaterial* d_mats = nullptr;
+    float4* d_node_aux = nullptr;
     DevNode* d_nodes = nullptr;
     DevTriHot* d_hot = nullptr;
     DevTriCold* d_cold = nullptr;
@@ -699,6 +701,9 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 2: launch_bounce_t<FIRST, HAS_BVH, 2>(grid, in, out, b); break;
         case 6: launch_bounce_t<FIRST, HAS_BVH, 6>(grid, in, out, b); break;
         case 10: launch_bounce_t<FIRST, HAS_BVH, 10>(grid, in, out, b); break;
+        case 18: launch_bounce_t<FIRST, HAS_BVH, 18>(grid, in, out, b); break;
+        case 26: launch_bounce_t<FIRST, HAS_BVH, 26>(grid, in, out, b); break;
+        case 22: launch_bounce_t<FIRST, HAS_BVH, 22>(grid, in, out, b); break;
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -737,7 +742,7 @@ int enqueue_pass_body(int batch) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 15, dim3(nb), in, out, b);
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 31, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -752,10 +757,12 @@ int enqueue_pass_body(int batch) {
         // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
         const int* n_in = g.opts.stream_compaction ? staged_count(b) : staged_count(0);
         HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
-        if (g.has_bvh)
-            launch(1, k_intersect<true>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
+        if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
+            launch(1, k_intersect<true, true>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
+        else if (g.has_bvh)
+            launch(1, k_intersect<true, false>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
         else
-            launch(1, k_intersect<false>, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, n_in);
+            launch(1, k_intersect<false, false>, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, n_in);
         HIPCHK(hipGetLastError());
         const int* perm = nullptr;
         if (g.opts.material_sort) {
@@ -844,7 +851,7 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
+    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
                     g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -952,7 +959,8 @@ void pt_default_options(pt_options* o) {
     o->shard_count = 1;
     o->shard_rows = 8;
     o->block_size = BLOCK;
-    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST;   // fastest in the in-process A/B (tools/ab_variants.py)
+    // fastest in the in-process A/B (tools/ab_variants.py); every variant is bit-identical
+    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST;
     o->frames_per_pass = 0;        // auto
 }
 
@@ -1108,6 +1116,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     // BVH: only when the reference would traverse it (BVH_ACCELERATION and a non-empty tree)
     g.has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
     std::vector<DevNode> nodes;
+    std::vector<float4> node_aux;
     std::vector<DevTriHot> hot;
     std::vector<DevTriCold> cold;
     if (g.has_bvh) {
@@ -1126,6 +1135,85 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             memcpy(&fb, &b, 4);
             nodes[i].lo = make_float4(nd.aabb.min.x, nd.aabb.min.y, nd.aabb.min.z, fa);
             nodes[i].hi = make_float4(nd.aabb.max.x, nd.aabb.max.y, nd.aabb.max.z, fb);
+        }
+        // per-node culling bounds and the reference's DFS visit rank (push left, push right, pop)
+        node_aux.assign(s->num_bvh_nodes, make_float4(0.f, 0.f, 0.f, 0.f));
+        {
+            double extent = std::max({1.0, std::fabs((double)s->camera.position.x),
+                                      std::fabs((double)s->camera.position.y), std::fabs((double)s->camera.position.z)});
+            for (int t = 0; t < s->num_triangles; ++t) {
+                const pt_vertex* v[3] = {&s->triangles[t].v1, &s->triangles[t].v2, &s->triangles[t].v3};
+                for (auto* x : v)
+                    extent = std::max({extent, std::fabs((double)x->position.x), std::fabs((double)x->position.y),
+                                       std::fabs((double)x->position.z)});
+            }
+            for (int i = 0; i < s->num_geoms; ++i)   // hit points on primitives are ray origins too
+                for (int r = 0; r < 3; ++r)
+                    extent = std::max(extent, std::fabs((double)geoms[i].box_lo[r]) + std::fabs((double)geoms[i].box_hi[r]));
+            std::vector<double> smax(s->num_bvh_nodes, -1.0);
+            // bottom-up max edge: children have larger indices than parents in the reference build,
+            // but compute it by explicit post-order to accept any valid tree
+            std::vector<int> order, st{0};
+            std::vector<char> seen(s->num_bvh_nodes, 0);
+            while (!st.empty()) {
+                int n = st.back();
+                st.pop_back();
+                if (n < 0 || n >= s->num_bvh_nodes || seen[n]) continue;
+                seen[n] = 1;
+                order.push_back(n);
+                const pt_bvh_node& nd = s->bvh_nodes[n];
+                if (!(nd.triCount > 0 && nd.start >= 0)) {
+                    if (nd.left >= 0) st.push_back(nd.left);
+                    if (nd.right >= 0) st.push_back(nd.right);
+                }
+            }
+            for (size_t k = order.size(); k-- > 0;) {
+                const int n = order[k];
+                const pt_bvh_node& nd = s->bvh_nodes[n];
+                double m = 0.0;
+                if (nd.triCount > 0 && nd.start >= 0) {
+                    for (int i = 0; i < nd.triCount; ++i) {
+                        const int ti = s->tri_indices[nd.start + i];
+                        if (ti < 0 || ti >= s->num_triangles) continue;   // rejected below
+                        const pt_triangle& t = s->triangles[ti];
+                        const double e1 = std::hypot((double)t.v2.position.x - t.v1.position.x,
+                                                     (double)t.v2.position.y - t.v1.position.y,
+                                                     (double)t.v2.position.z - t.v1.position.z);
+                        const double e2 = std::hypot((double)t.v3.position.x - t.v1.position.x,
+                                                     (double)t.v3.position.y - t.v1.position.y,
+                                                     (double)t.v3.position.z - t.v1.position.z);
+                        m = std::max({m, e1, e2});
+                    }
+                } else {
+                    if (nd.left >= 0) m = std::max(m, smax[nd.left]);
+                    if (nd.right >= 0) m = std::max(m, smax[nd.right]);
+                }
+                smax[n] = m;
+                const double sx = m * 1.01 + 1e-30;
+                const double c = 64.0 * std::ldexp(1.0, -24) * sx * sx / 1e-5;
+                node_aux[n].x = (float)std::min(c * 1.01, 1e30);
+                node_aux[n].y = (float)std::min(sx, 1e30);
+                node_aux[n].w = (float)std::min(c * extent * 1.01, 1e30);
+            }
+            // reference visit rank
+            int rank = 0;
+            st.assign(1, 0);
+            std::fill(seen.begin(), seen.end(), 0);
+            while (!st.empty()) {
+                int n = st.back();
+                st.pop_back();
+                if (n < 0 || n >= s->num_bvh_nodes) continue;
+                int r = rank++;
+                float fr;
+                memcpy(&fr, &r, 4);
+                node_aux[n].z = fr;
+                const pt_bvh_node& nd = s->bvh_nodes[n];
+                if (!(nd.triCount > 0 && nd.start >= 0) && !seen[n]) {
+                    seen[n] = 1;
+                    if (nd.left >= 0) st.push_back(nd.left);
+                    if (nd.right >= 0) st.push_back(nd.right);
+                }
+            }
         }
         hot.resize(s->num_tri_indices);
         for (int k = 0; k < s->num_tri_indices; ++k) {
@@ -1170,6 +1258,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     RC(upload(g.d_mats, mats.data(), mats.size()));
     if (g.has_bvh) {
         RC(dalloc(&g.d_nodes, nodes.size()));
+        RC(dalloc(&g.d_node_aux, node_aux.size()));
+        RC(upload(g.d_node_aux, node_aux.data(), node_aux.size()));
         RC(dalloc(&g.d_hot, hot.size()));
         RC(dalloc(&g.d_cold, cold.size()));
         RC(upload(g.d_nodes, nodes.data(), nodes.size()));
@@ -1222,6 +1312,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.geoms = g.d_geoms;
     sc.mats = g.d_mats;
     sc.nodes = g.d_nodes;
+    sc.node_aux = g.d_node_aux;
     sc.hot = g.d_hot;
     sc.cold = g.d_cold;
     sc.num_geoms = s->num_geoms;
@@ -1378,12 +1469,15 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     RC(upload_paths(0, paths, n));
     RC(set_count(0, (int)n));
     HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
-    if (g.has_bvh)
-        hipLaunchKernelGGL((k_intersect<true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
+    if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
+        hipLaunchKernelGGL((k_intersect<true, true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
+                           pathbuf(0), hits, staged_count(0));
+    else if (g.has_bvh)
+        hipLaunchKernelGGL((k_intersect<true, false>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
                            pathbuf(0), hits, staged_count(0));
     else
-        hipLaunchKernelGGL((k_intersect<false>), dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0),
-                           hits, staged_count(0));
+        hipLaunchKernelGGL((k_intersect<false, false>), dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc,
+                           pathbuf(0), hits, staged_count(0));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g.stream));
     std::vector<float4> nt(n);

@@ -86,10 +86,12 @@ def _oracle_isects(oracle, a, paths):
     return out
 
 
-@pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy", "cornell_obj_khaslana", "synthetic_textured_bump"])
-def test_intersect_bitexact(name, oracle, ptamd):
+@pytest.mark.parametrize("name,variant", [("cornell", 10), ("cornell_obj_bnnuy", 10), ("cornell_obj_khaslana", 10),
+                                          ("synthetic_textured_bump", 10), ("cornell_obj_bnnuy", 26),
+                                          ("cornell_obj_khaslana", 26), ("synthetic_textured_bump", 26)])
+def test_intersect_bitexact(name, variant, oracle, ptamd):
     a, b = _oracle_pair(oracle, ptamd, name, (96, 96))      # wavefront capacity >= 9216 paths
-    tr = ptamd.PathTracer(b)
+    tr = ptamd.PathTracer(b, variant=variant)
     paths = _random_paths(3000, 11)
     cam = tr.test_camera(3)[:4000]
     paths = np.concatenate([paths.astype(oracle.PATH), cam])
@@ -185,6 +187,10 @@ FRAME_CASES = [
     ("cornell_glass_test", (64, 64), None, {"variant": 10}),
     ("cornell_obj_bnnuy", (48, 48), None, {"variant": 10}),
     ("synthetic_textured_bump", (48, 48), None, {"variant": 10}),
+    ("cornell_obj_bnnuy", (64, 64), None, {"variant": 26}),             # fast BVH traversal
+    ("cornell_obj_bnnuy", (64, 64), None, {"variant": 18, "pipeline": 1}),
+    ("cornell_obj_khaslana", (48, 48), 12, {"variant": 26}),
+    ("synthetic_textured_bump", (48, 48), None, {"variant": 26}),
     ("synthetic_textured_bump", (64, 64), None, {"pipeline": 1}),
     ("synthetic_textured_bump", (48, 48), None, {"pipeline": 1, "material_sort": 1}),
     ("cornell_obj_phatphuck_texture_test", (48, 48), None, {}),
@@ -278,6 +284,21 @@ def test_full_resolution_cornell(oracle, ptamd):
         imgs.append(tr.image())
         tr.free()
     assert _eq(imgs[0], r.image) and _eq(imgs[1], r.image)
+
+
+@pytest.mark.parametrize("name", ["cornell_obj_bnnuy", "cornell_obj_khaslana"])
+def test_full_resolution_mesh_fast_bvh(name, oracle, ptamd):
+    """800x800 frames of the BVH scenes with the fast traversal (variant 26): bit-exact vs the
+    oracle's reference-order DFS, live counts included."""
+    a, b = _oracle_pair(oracle, ptamd, name, None)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr = ptamd.PathTracer(b, variant=26)
+    for it in (1, 2):
+        live = r.trace(it)
+        tr.trace(it)
+        assert tr.stats()["live"] == [int(x) if x >= 0 else 0 for x in live]
+    assert _eq(tr.image(), r.image)
+    tr.free()
 
 
 def test_graph_replay_equals_eager(oracle, ptamd):

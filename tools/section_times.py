@@ -39,7 +39,10 @@ def main():
            "exact_tests_per_live_lane": round(c["n_exact"] / lanes, 3),
            "candidates_per_live_lane": round(c["n_cand"] / lanes, 3),
            "loop_iters_per_wave": round(c["n_iters"] / max(1, c["n_waves"]), 3),
-           "live_lanes_per_wave": round(lanes / max(1, c["n_waves"]), 2), "raw": c}
+           "live_lanes_per_wave": round(lanes / max(1, c["n_waves"]), 2),
+           "bvh_nodes_per_ray": round(c["n_nodes"] / max(1, c["n_bvh_rays"]), 2),
+           "bvh_tris_per_ray": round(c["n_tris"] / max(1, c["n_bvh_rays"]), 2),
+           "aabb_decision_mismatches": c["n_aabb_mismatch"], "raw": c}
     print(json.dumps(out, indent=1))
     tr.free()
 
