@@ -75,8 +75,11 @@ typedef struct pt_options {
                                     2: per-lane candidate queue for the geom tests, 4: section
                                     timing (tools), 8: exact geom tests redistributed over the
                                     wave's lanes, 16: BVH traversal with exact-decision fast box
-                                    tests, near-first order and certified t-culling); results are
-                                    bit-identical for every value.  Default 2|8|16 */
+                                    tests, near-first order and certified t-culling, 32: rays
+                                    that enter the mesh's root box are queued and traversed in
+                                    full waves by a second kernel per bounce, 64: keep 16 on the
+                                    reference node array instead of the paired-children layout);
+                                    results are bit-identical for every value.  Default 2|8|16|32 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..16;
                                     0 = auto: ~5.2M paths in flight).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in

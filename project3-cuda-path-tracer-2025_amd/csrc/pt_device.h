@@ -126,6 +126,20 @@ struct DevNode {
     float4 hi;
 };
 
+// The two children of one internal BVH node, 64 bytes (VAR_BVH_FAST layout): popping a node
+// costs ONE dependent record fetch that holds both child boxes and everything needed to push
+// them.  ref >= 0 names the child's own pair record when ref < num_pairs, else the leaf
+// ref - num_pairs, whose triangles sit in the 4-slot group hot4[4 * leaf ..]; leaves are numbered
+// in the reference's visit order (push left, push right, pop: right subtree first), so a smaller
+// hot4 index is an earlier triangle in the reference's DFS.  s = max triangle edge below the
+// child (x 1.01), the size term of the certified t-cull.
+struct DevPair {
+    float4 l_lo;   // left box min.xyz  | left ref (int bits)
+    float4 l_hi;   // left box max.xyz  | left s
+    float4 r_lo;   // right box min.xyz | right ref (int bits)
+    float4 r_hi;   // right box max.xyz | right s
+};
+
 // hot triangle record in leaf order (index k = node.start + i): 3 positions, 48 bytes
 struct DevTriHot {
     float4 a;   // v0.xyz, v1.x

@@ -13,8 +13,8 @@
 
 namespace ptd {
 
-constexpr int NSEG = 8;
-constexpr int LDS_GEOMS = 64;  // fused kernel: geom tables up to this size are staged in LDS        // output segments of the fused compaction (one per XCD group)
+constexpr int NSEG = 8;        // output segments of the fused compaction (one per XCD group)
+constexpr int LDS_GEOMS = 64;  // fused kernel: geom tables up to this size are staged in LDS
 constexpr int MAXB = 64;       // max trace depth supported by the frame control block
 constexpr int BLOCK = 256;     // threads per block of the per-path kernels
 constexpr int MAXSTACK = 64;   // reference BVH stack (intersections.cu:167)
@@ -24,10 +24,13 @@ constexpr int CNT_PAD = 32;    // one 128-byte cache line per live counter (atom
 enum : int {
     VAR_WAVE_ATOMIC = 1,   // compaction: one atomic per wave, no block barrier
     VAR_CAND_QUEUE = 2,    // intersection: per-lane queue of candidate geoms (see intersect_scene_q)
-    VAR_SECTION_TIMING = 4,
+    VAR_SECTION_TIMING = 4,    // tools only: per-wave shader-clock section times into g_sections
     VAR_WAVE_REDIST = 8,   // intersection: the wave's (ray, candidate) pairs spread over all 64 lanes
     VAR_BVH_FAST = 16,     // BVH: exact-decision fast AABB test, near-first order, certified t-culling
-    VAR_CTILE8 = 16,       // staged compaction: 8 items per thread (2048-item tiles)// tools only: per-wave shader-clock section times into g_sections
+    VAR_CTILE8 = 16,       // staged compaction: 8 items per thread (2048-item tiles)
+    VAR_BVH_SPLIT = 32,    // fused + BVH_FAST + pair layout: rays that enter the mesh's root box are
+                           // queued and traversed (then shaded) by k_bvh_bounce in full waves
+    VAR_BVH_NODES = 64,    // host only: BVH_FAST on the node array instead of the DevPair layout (A/B)
 };
 
 struct CamDev {
@@ -58,6 +61,13 @@ struct SceneDev {
     const uint32_t* texels;   // all textures' RGBA8 texels, concatenated
     const int4* texinfo;      // per texture: texel offset, width, height
     int num_textures;
+    // VAR_BVH_FAST layout (pairs != null when the tree allows it, see DevPair)
+    const DevPair* pairs;
+    const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
+    int num_pairs, root_ref;
+    float4 root_lo, root_hi;  // root box (w: root s)
+    float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
+    float cull_E;             // scene extent (rounded up): cE = c * cull_E
 };
 
 // frame control block (device memory); zeroed / advanced by k_frame_begin every frame
@@ -68,12 +78,13 @@ struct FrameCtl {
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
+    int qcnt[MAXB + 1][CNT_PAD];            // VAR_BVH_SPLIT: paths of bounce b queued for traversal
 };
 
 // VAR_SECTION_TIMING (tools/section_times.py): wave-level s_memtime deltas per kernel section and
 // per-lane work counters, summed by the first active lane of each wave
 enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
-       SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_COUNT };
+       SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS, SEC_COUNT };
 __device__ unsigned long long g_sections[16];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
 PT_DEV void sec_add(int k, uint64_t v) {
@@ -162,7 +173,7 @@ struct Hit {
 // slot (index into the leaf-ordered hot triangle array) in `btri`.
 template <bool COUNT = false>
 PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& bu, float& bv, int& btri) {
-    int n_nodes = 0, n_tris = 0, n_it = 0;
+    int n_nodes = 0, n_tris = 0;
     float t_hit = FLT_MAX_;
     bool hit = false;
     btri = -1;
@@ -170,6 +181,7 @@ PT_DEV float bvh_intersect(const SceneDev& sc, f3 ro, f3 rd, int* stack, float& 
     stack[0] = 0;
     sp = 1;
     while (sp > 0) {
+        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
         int ni = stack[(--sp) * BLOCK];
         DevNode nd = sc.nodes[ni];
         if (COUNT) n_nodes++;
@@ -276,6 +288,7 @@ PT_DEV float bvh_intersect_fast(const SceneDev& sc, f3 ro, f3 rd, int* stack, fl
     stack[0] = packed ? (int)pack_entry(0, e0) : 0;
     sp = 1;
     while (sp > 0) {
+        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
         const uint32_t w = (uint32_t)stack[(--sp) * BLOCK];
         const int ni = packed ? (int)(w >> 16) : (int)w;
         const float t_best = __builtin_fminf(t_hit, t_limit);
@@ -336,6 +349,124 @@ PT_DEV float bvh_intersect_fast(const SceneDev& sc, f3 ro, f3 rd, int* stack, fl
     return hit ? t_hit : -1.f;
 }
 
+// VAR_BVH_FAST on the pair layout: the same visited-node decisions, cull bound and tie rule as
+// bvh_intersect_fast, restructured for fewer dependent fetches.
+//  * the node being expanded is a 64-B DevPair of its children: one record fetch yields both
+//    boxes (exact-decision aabb_decide), their refs and their cull sizes;
+//  * the nearer accepted child is expanded next without touching the stack; the farther one is
+//    pushed as [ref:16 | T:bf16], where T is the cull threshold of node_culled solved for t_best
+//    (culled iff t_best < T, T rounded down), so a pop needs no fetch to decide the cull;
+//  * leaf triangles live in 4-slot groups in reference visit order: ties on t go to the smaller
+//    hot4 index, i.e. to the triangle the reference meets first.
+// node_culled(entry, {c, s, ., cE}, t): entry(1-1e-6) > t(1 + c(2 + 1.001 s/t) + 1e-6) + cE
+//   <=> t < (entry(1-1e-6) - 1.001 c s - cE) / (1 + 2c + 1e-6); evaluated with extra 1e-6 slack
+//   on each side for the float rounding of this rearrangement.
+PT_DEV float cull_threshold(const SceneDev& sc, float entry, float s) {
+    const float c = (s * s) * sc.cull_c0;
+    const float num = entry * (1.0f - 2e-6f) - (c * s * 1.002f + c * sc.cull_E * (1.0f + 1e-6f));
+    const float T = num * __builtin_amdgcn_rcpf(1.0f + 2.0f * c + 2e-6f) * (1.0f - 1e-6f);
+    return T > 0.0f ? T : 0.0f;      // NaN (inf - inf on degenerate data) -> 0: never culled
+}
+PT_DEV uint32_t pack_ref(int ref, float T) { return ((uint32_t)ref << 16) | (__float_as_uint(T) >> 16); }
+
+template <bool COUNT = false>
+PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
+                                 int& btri) {
+    int n_nodes = 0, n_tris = 0;
+    const bool exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
+                         rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);   // NaN / inf ray
+    const f3 rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    float t_hit = FLT_MAX_;
+    btri = 0x7fffffff;
+    float e0;
+    if (!aabb_decide(sc.root_lo, sc.root_hi, ro, rd, rr, exact, e0)) return -1.f;
+    if (t_limit < cull_threshold(sc, e0, sc.root_hi.w)) return -1.f;
+    const int P = sc.num_pairs;
+    int cur = sc.root_ref;
+    int sp = 0;
+    while (true) {
+        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
+        const float t_best = __builtin_fminf(t_hit, t_limit);
+        bool next = false;
+        if (cur < P) {
+            if (COUNT) n_nodes++;
+            const DevPair pr = sc.pairs[cur];
+            float el = 0.f, er = 0.f;
+            bool pl = aabb_decide(pr.l_lo, pr.l_hi, ro, rd, rr, exact, el);
+            bool pb = aabb_decide(pr.r_lo, pr.r_hi, ro, rd, rr, exact, er);
+            const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
+            const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
+            pl = pl && !(t_best < Tl);
+            pb = pb && !(t_best < Tr);
+            const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
+            if (pl && pb) {
+                const bool lfirst = el <= er;
+                cur = lfirst ? rl : rrf;
+                const int far = lfirst ? rrf : rl;
+                const float Tf = lfirst ? Tr : Tl;
+                if (sp < sc.stack_depth) stack[(sp++) * BLOCK] = (int)pack_ref(far, Tf);
+                next = true;
+            } else if (pl | pb) {
+                cur = pl ? rl : rrf;
+                next = true;
+            }
+        } else {
+            const int base = 4 * (cur - P);
+            const DevTriHot t0 = sc.hot4[base];
+            const int cnt = __float_as_int(t0.c.z);
+            if (COUNT) { n_nodes++; n_tris += cnt; }
+            for (int i = 0; i < cnt; ++i) {
+                const DevTriHot th = i == 0 ? t0 : sc.hot4[base + i];
+                const f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+                const f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+                const f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+                float t, u, v;
+                if (tri_test(ro, rd, v0, v1, v2, t, u, v) && t > 0.0f &&
+                    (t < t_hit || (t == t_hit && base + i < btri))) {
+                    t_hit = t;
+                    bu = u;
+                    bv = v;
+                    btri = base + i;
+                }
+            }
+        }
+        if (!next) {
+            const float tb = __builtin_fminf(t_hit, t_limit);
+            cur = -1;
+            while (sp > 0) {
+                const uint32_t w = (uint32_t)stack[(--sp) * BLOCK];
+                if (!(tb < __uint_as_float(w << 16))) {
+                    cur = (int)(w >> 16);
+                    break;
+                }
+            }
+            if (cur < 0) break;
+        }
+    }
+    if (COUNT) {
+        sec_add_lanes(SEC_N_NODES, n_nodes);
+        sec_add_lanes(SEC_N_TRIS, n_tris);
+        sec_add_lanes(SEC_N_BVH_RAYS, 1);
+    }
+    if (t_hit == FLT_MAX_) {
+        btri = -1;
+        return -1.f;
+    }
+    return t_hit;
+}
+
+// VAR_BVH_SPLIT: does bvh_intersect_pairs do anything for this ray beyond its root test?  The
+// same root decision and root cull as bvh_intersect_pairs; false means the mesh cannot change the
+// primitive winner (t_limit), true means the ray is queued for k_bvh_bounce.
+PT_DEV bool bvh_root_needed(const SceneDev& sc, f3 ro, f3 rd, float t_limit) {
+    const bool exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
+                         rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);
+    const f3 rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    float e0;
+    if (!aabb_decide(sc.root_lo, sc.root_hi, ro, rd, rr, exact, e0)) return false;
+    return !(t_limit < cull_threshold(sc, e0, sc.root_hi.w));
+}
+
 // Conservative pre-test of one geom (approximate arithmetic, never decides a result): true
 // when the exact test is CERTAIN not to update (t_min, winner) — the ray line misses the geom's
 // margin-expanded world box, or enters it farther than t_min.  Slabs as fma(bound, 1/d, -o/d)
@@ -374,7 +505,7 @@ PT_DEV bool cull_geom(const DevGeom& g, const CullRay& c, float t_min) {
 // miss / facing conventions of pathtrace.cu:397-446
 template <bool HAS_BVH, bool BVH_FAST = false, bool COUNT = false>
 PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
-                      f3 seed) {
+                      f3 seed, bool traverse = true) {
     Hit h;
     h.tri = -1;
     h.u = 0.f;
@@ -389,15 +520,17 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
         mat = g.materialid;
     }
     if (HAS_BVH) {
-        if (sc.use_bvh && sc.num_nodes > 0) {
+        if (traverse && sc.use_bvh && sc.num_nodes > 0) {
             float u, v;
             int tri;
-            float tb = BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
+            const bool pairs = BVH_FAST && sc.pairs != nullptr;
+            float tb = pairs ? bvh_intersect_pairs<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
+                     : BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
                                 : bvh_intersect<COUNT>(sc, ro, rd, stack, u, v, tri);
             if (tb > 0.0f && tb < t_min) {
                 t_min = tb;
                 hit_index = -2;
-                DevTriHot th = sc.hot[tri];          // bvh_intersect returns the leaf slot
+                DevTriHot th = (pairs ? sc.hot4 : sc.hot)[tri];   // traversal returns the slot
                 int tri_index = __float_as_int(th.c.y);
                 const DevTriCold& cd = sc.cold[tri_index];
                 mat = cd.materialID;
@@ -461,17 +594,18 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
 // and re-checks the cull against its current t_min before the exact test.  The wave executes
 // max-over-lanes(candidates) exact tests instead of one per geom any lane needs.
 // `lgeoms`: the block's LDS copy of the geom table (the caller's job; sc.num_geoms <= 64).
-template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false>
-PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
+template <bool TIMING = false>
+PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, float& t_min, int& win,
+                             f3& seed) {
     uint64_t tc0 = TIMING ? sec_clock() : 0;
     const CullRay cr = cull_ray(ro, rd);
     uint64_t cand = 0;
 #pragma unroll 4
     for (int i = 0; i < sc.num_geoms; ++i)
         if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
-    float t_min = FLT_MAX_;
-    int win = -1;
-    f3 seed = mk(0.f, 0.f, 0.f);
+    t_min = FLT_MAX_;
+    win = -1;
+    seed = mk(0.f, 0.f, 0.f);
     int n_exact = 0, n_iters = 0;
     uint64_t tc1 = 0;
     if (TIMING) {
@@ -498,10 +632,19 @@ PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
         }
     }
     if (TIMING) {
-        uint64_t tc2 = sec_clock();
-        sec_add(SEC_EXACT, tc2 - tc1);
+        sec_add(SEC_EXACT, sec_clock() - tc1);
         sec_add_lanes(SEC_N_EXACT, n_exact);
         sec_add(SEC_N_ITERS, (uint64_t)n_iters);
+    }
+}
+template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false>
+PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
+    float t_min;
+    int win;
+    f3 seed;
+    prim_intersect_q<TIMING>(sc, lgeoms, ro, rd, t_min, win, seed);
+    if (TIMING) {
+        const uint64_t tc2 = sec_clock();
         Hit h = finish_hit<HAS_BVH, BVH_FAST, true>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
         sec_add(SEC_FINISH, sec_clock() - tc2);
         return h;

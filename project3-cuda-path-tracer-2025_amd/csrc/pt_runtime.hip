@@ -50,6 +50,7 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
     }
     __syncthreads();
     for (int i = t; i < (MAXB + 1) * NSEG * CNT_PAD; i += blockDim.x) (&ctl->cnt[0][0][0])[i] = 0;
+    for (int i = t; i < (MAXB + 1) * CNT_PAD; i += blockDim.x) (&ctl->qcnt[0][0])[i] = 0;
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
@@ -109,14 +110,50 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
 // --------------------------------------------------------------------------------------------
 // FUSED: camera (bounce 0) | load -> intersect -> shade -> gather dead -> compact survivors
 // --------------------------------------------------------------------------------------------
+// VAR_BVH_SPLIT traversal queue: the path (3 float4 as in PathBuf, C.w = frame slot | (winner
+// geom + 1) << 8) and the primitive result it enters traversal with (t_min, normal seed)
+struct QueueBuf {
+    float4 *A, *B, *C, *D;   // D = t_min | seed.xyz
+};
+
+// Block-aggregated append of up to two flags: ballot -> per-wave counts -> one atomic per flag
+// per block (counters on their own cache lines).  Returns each flagged lane's index.  Every
+// thread of the block must call it.
+template <bool TWO>
+PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i1) {
+    __shared__ int s_w[2][BLOCK / 64];
+    __shared__ int s_b[2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t m0 = __ballot(f0);
+    const uint64_t m1 = TWO ? __ballot(f1) : 0ull;
+    if (lane == 0) {
+        s_w[0][w] = __popcll(m0);
+        if (TWO) s_w[1][w] = __popcll(m1);
+    }
+    __syncthreads();
+    if (tid < (TWO ? 2 : 1)) {
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) {
+            const int c = s_w[tid][i];
+            s_w[tid][i] = tot;
+            tot += c;
+        }
+        s_b[tid] = tot ? atomicAdd(tid == 0 ? ctr0 : ctr1, tot) : 0;
+    }
+    __syncthreads();
+    i0 = s_b[0] + s_w[0][w] + mbcnt(m0);
+    i1 = TWO ? s_b[1] + s_w[1][w] + mbcnt(m1) : 0;
+}
+
 template <bool FIRST, bool HAS_BVH, int VAR>
 __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
-                                                  float* __restrict__ image, int bounce, int seg_stride) {
+                                                  float* __restrict__ image, int bounce, int seg_stride,
+                                                  QueueBuf q) {
     // dynamic LDS: [geom table, sc.num_geoms <= LDS_GEOMS, candidate-queue variants]
-    //              [HAS_BVH: traversal stack, stack_depth x BLOCK ints]
+    //              [HAS_BVH && !SPLIT: traversal stack, stack_depth x BLOCK ints]
+    //              [VAR_WAVE_REDIST: one WaveLds per wave]
     extern __shared__ float4 s_dyn[];
-    __shared__ int s_wave[BLOCK / 64];
-    __shared__ int s_base;
     const int iter = ctl->iter;
     const int batch = ctl->batch;
     int n;
@@ -135,12 +172,15 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     constexpr bool QUEUE = (VAR & VAR_CAND_QUEUE) != 0;
     constexpr bool REDIST = (VAR & VAR_WAVE_REDIST) != 0;
     constexpr bool BVH_FAST = (VAR & VAR_BVH_FAST) != 0;
+    // split: the launcher guarantees the pair layout and an LDS geom table (queue or redist)
+    constexpr bool SPLIT = HAS_BVH && BVH_FAST && (VAR & VAR_BVH_SPLIT) && (QUEUE || REDIST) && !TIMING;
     uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
     const bool lds_geoms = (QUEUE || REDIST) && sc.num_geoms <= LDS_GEOMS;
     DevGeom* s_geoms = reinterpret_cast<DevGeom*>(s_dyn);
     int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? sc.num_geoms * (int)(sizeof(DevGeom) / 16) : 0));
-    WaveLds* s_wave_isect = reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
+    WaveLds* s_wave_isect =
+        reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH && !SPLIT ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
     if (lds_geoms) {   // per-lane candidate tests then read their geom from LDS, not L2
         const float4* src = reinterpret_cast<const float4*>(sc.geoms);
         for (int k = tid; k < sc.num_geoms * (int)(sizeof(DevGeom) / 16); k += BLOCK) s_dyn[k] = src[k];
@@ -192,55 +232,115 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     }
     const bool live = active && p.rb > 0;
     Hit h;
+    bool queued = false;
+    float qt = 0.f;
+    int qw = -1;
+    f3 qs = mk(0.f, 0.f, 0.f);
     if (REDIST && lds_geoms) {                     // wave-cooperative: every lane takes part
-        float wt;
-        int ww;
-        f3 ws;
-        wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, wt, ww, ws);
-        if (live) h = finish_hit<HAS_BVH, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid, wt, ww, ws);
+        wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
+    } else if (SPLIT && live) {
+        prim_intersect_q(sc, s_geoms, p.o, p.d, qt, qw, qs);
     }
     if (live) {
-        if (!(REDIST && lds_geoms))
+        if (SPLIT) {
+            queued = bvh_root_needed(sc, p.o, p.d, qt);
+            if (!queued) h = finish_hit<false>(sc, s_geoms, p.o, p.d, s_stack + tid, qt, qw, qs);
+        } else if (REDIST && lds_geoms) {
+            h = finish_hit<HAS_BVH, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid, qt, qw, qs);
+        } else {
             h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
-        uint64_t ts = TIMING ? sec_clock() : 0;
-        shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
-        if (TIMING) {
-            tc = sec_clock();
-            sec_add(SEC_SHADE, tc - ts);
+        }
+        if (!queued) {
+            uint64_t ts = TIMING ? sec_clock() : 0;
+            shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+            if (TIMING) {
+                tc = sec_clock();
+                sec_add(SEC_SHADE, tc - ts);
+            }
         }
     }
     if (TIMING && active) tc = sec_clock();
-    const bool surv = active && p.rb > 0;
-    if (active && !surv) gather_into_image(image, sc, batch, p);
-    const uint64_t m = __ballot(surv);
-    const int lane = tid & 63, w = tid >> 6;
+    const bool surv = active && !queued && p.rb > 0;
+    if (active && !queued && !surv) gather_into_image(image, sc, batch, p);
+    const int lane = tid & 63;
     const int seg = blockIdx.x & (NSEG - 1);
     if (VAR & VAR_WAVE_ATOMIC) {
         // one returning atomic per wave on a counter that owns its cache line; no barrier
-        if (m == 0) return;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&ctl->cnt[bounce + 1][seg][0], __popcll(m));
-        base = __shfl(base, 0);
-        if (surv) store_path(out, seg * seg_stride + base + mbcnt(m), p);
+        const uint64_t m = __ballot(surv);
+        if (m != 0) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&ctl->cnt[bounce + 1][seg][0], __popcll(m));
+            base = __shfl(base, 0);
+            if (surv) store_path(out, seg * seg_stride + base + mbcnt(m), p);
+        }
+        if (!SPLIT) return;
+        const uint64_t mq = __ballot(queued);
+        if (mq != 0) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&ctl->qcnt[bounce][0], __popcll(mq));
+            base = __shfl(base, 0);
+            if (queued) {
+                const int k = base + mbcnt(mq);
+                q.A[k] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+                q.B[k] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+                q.C[k] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
+                q.D[k] = make_float4(qt, qs.x, qs.y, qs.z);
+            }
+        }
         return;
     }
-    // block-aggregated compaction: ballot -> per-wave counts -> one atomic per block
-    if (lane == 0) s_wave[w] = __popcll(m);
-    __syncthreads();
-    if (tid == 0) {
-        int tot = 0;
-#pragma unroll
-        for (int i = 0; i < BLOCK / 64; ++i) {
-            int c = s_wave[i];
-            s_wave[i] = tot;
-            tot += c;
-        }
-        s_base = tot ? seg * seg_stride + atomicAdd(&ctl->cnt[bounce + 1][seg][0], tot) : 0;
+    // block-aggregated compaction (+ the traversal queue): one atomic per counter per block
+    int si, qi;
+    block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][0], si, qi);
+    if (surv) store_path(out, seg * seg_stride + si, p);
+    if (SPLIT && queued) {
+        q.A[qi] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+        q.B[qi] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+        q.C[qi] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
+        q.D[qi] = make_float4(qt, qs.x, qs.y, qs.z);
     }
-    __syncthreads();
-    if (surv) store_path(out, s_base + s_wave[w] + mbcnt(m), p);
     if (TIMING && active) sec_add(SEC_STORE, sec_clock() - tc);
+}
+
+// VAR_BVH_SPLIT, second half of a bounce: the queued paths, 64 to a wave, traverse the mesh
+// (bvh_intersect_pairs via finish_hit, entering with their primitive winner), are shaded, and
+// gathered / compacted into the same output segments as k_bounce (blockIdx % NSEG; the host
+// doubles seg_stride so both kernels' survivors fit).
+template <int VAR>
+__global__ __launch_bounds__(BLOCK) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
+                                                      float* __restrict__ image, int bounce, int seg_stride) {
+    extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
+    const int n = ctl->qcnt[bounce][0];
+    const int block_start = blockIdx.x * BLOCK;
+    if (block_start >= n) return;
+    const int iter = ctl->iter;
+    const int batch = ctl->batch;
+    const int tid = threadIdx.x;
+    const int gid = block_start + tid;
+    const bool active = gid < n;
+    PathReg p;
+    p.rb = 0;
+    if (active) {
+        const float4 a = q.A[gid], b = q.B[gid], c = q.C[gid], d = q.D[gid];
+        p.o = mk(a.x, a.y, a.z);
+        p.pix = __float_as_int(a.w);
+        p.d = mk(b.x, b.y, b.z);
+        p.rb = __float_as_int(b.w);
+        p.c = mk(c.x, c.y, c.z);
+        const int cw = __float_as_int(c.w);
+        p.slot = cw & 255;
+        const int win = (cw >> 8) - 1;
+        const Hit h = finish_hit<true, true>(sc, sc.geoms, p.o, p.d, reinterpret_cast<int*>(s_dyn) + tid, d.x, win,
+                                             mk(d.y, d.z, d.w));
+        shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+    }
+    const bool surv = active && p.rb > 0;
+    if (active && !surv) gather_into_image(image, sc, batch, p);
+    const int seg = blockIdx.x & (NSEG - 1);
+    int si, unused;
+    block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
+    if (surv) store_path(out, seg * seg_stride + si, p);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -620,6 +720,8 @@ struct State {
     float4* d_node_aux = nullptr;
     DevNode* d_nodes = nullptr;
     DevTriHot* d_hot = nullptr;
+    DevPair* d_pairs = nullptr;
+    DevTriHot* d_hot4 = nullptr;
     DevTriCold* d_cold = nullptr;
     float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     float4* d_hit_nt = nullptr;
@@ -637,6 +739,8 @@ struct State {
     FrameCtl* d_ctl = nullptr;
     float* d_contrib = nullptr;      // passes of F > 1 frames: F planes of pixels_total float3
     int batch = 1;                   // frames per pass (pt_options.frames_per_pass, resolved)
+    bool split = false;              // VAR_BVH_SPLIT active (fused, fast BVH on the pair layout)
+    QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
     hipGraphExec_t graph_exec[MAXF + 1] = {};
@@ -687,11 +791,16 @@ const int* staged_count(int b) { return &g.d_ctl->cnt[b][0][0]; }
 
 template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
+    constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
     const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && g.sc.num_geoms <= LDS_GEOMS;
     const size_t geom_lds = lds ? sizeof(DevGeom) * g.sc.num_geoms : 0;
     const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds ? sizeof(WaveLds) * (BLOCK / 64) : 0;
-    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + (HAS_BVH ? g.bvh_lds : 0) + redist_lds, g.sc, in, out,
-           g.d_ctl, g.d_image, b, g.seg_stride);
+    const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + redist_lds, g.sc, in, out,
+           g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
+    if (SPLIT)
+        launch(100 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds, g.sc, g.queue, out, g.d_ctl, g.d_image, b,
+               g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -704,6 +813,8 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 18: launch_bounce_t<FIRST, HAS_BVH, 18>(grid, in, out, b); break;
         case 26: launch_bounce_t<FIRST, HAS_BVH, 26>(grid, in, out, b); break;
         case 22: launch_bounce_t<FIRST, HAS_BVH, 22>(grid, in, out, b); break;
+        case 50: launch_bounce_t<FIRST, HAS_BVH, 50>(grid, in, out, b); break;
+        case 58: launch_bounce_t<FIRST, HAS_BVH, 58>(grid, in, out, b); break;
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -711,6 +822,7 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     // camera rays of neighbouring pixels share their candidates: redistribution only costs there
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~VAR_WAVE_REDIST;
+    if (!g.split) var &= ~VAR_BVH_SPLIT;
     if (first) {
         if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
         else launch_bounce_v<true, false>(var, grid, in, out, b);
@@ -742,7 +854,7 @@ int enqueue_pass_body(int batch) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 31, dim3(nb), in, out, b);
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 63, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -851,8 +963,9 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
-                    g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl};
+    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
+                    g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl,
+                    g.queue.A, g.queue.B, g.queue.C, g.queue.D};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < 2; ++i)
@@ -960,7 +1073,7 @@ void pt_default_options(pt_options* o) {
     o->shard_rows = 8;
     o->block_size = BLOCK;
     // fastest in the in-process A/B (tools/ab_variants.py); every variant is bit-identical
-    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST;
+    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BVH_SPLIT;
     o->frames_per_pass = 0;        // auto
 }
 
@@ -1025,10 +1138,6 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         return fail(PT_E_INVALID, "frames_per_pass must be 0 (auto) .. %d", MAXF);
     g.batch = o.frames_per_pass > 0 ? o.frames_per_pass : auto_batch(g.local_pixels);
     if ((int64_t)g.local_pixels * g.batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
-    const int nb = nblocks(std::max(1, g.local_pixels * g.batch));
-    g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK;
-    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels * g.batch);
-    g.capacity = ((g.capacity + STILE - 1) / STILE) * STILE;   // tile-padded: kernels may read a whole tile
 
     // ---- scene -> device records ----
     std::vector<DevGeom> geoms(s->num_geoms);
@@ -1119,6 +1228,11 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     std::vector<float4> node_aux;
     std::vector<DevTriHot> hot;
     std::vector<DevTriCold> cold;
+    std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
+    std::vector<DevTriHot> hot4;
+    int pair_root_ref = 0, pair_count = 0;
+    float4 pair_root_lo{}, pair_root_hi{};
+    double cull_extent = 1.0;
     if (g.has_bvh) {
         nodes.resize(s->num_bvh_nodes);
         for (int i = 0; i < s->num_bvh_nodes; ++i) {
@@ -1150,6 +1264,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             for (int i = 0; i < s->num_geoms; ++i)   // hit points on primitives are ray origins too
                 for (int r = 0; r < 3; ++r)
                     extent = std::max(extent, std::fabs((double)geoms[i].box_lo[r]) + std::fabs((double)geoms[i].box_hi[r]));
+            cull_extent = extent;
             std::vector<double> smax(s->num_bvh_nodes, -1.0);
             // bottom-up max edge: children have larger indices than parents in the reference build,
             // but compute it by explicit post-order to accept any valid tree
@@ -1246,11 +1361,86 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             c.materialID = t.materialID;
         }
         g.stack_depth = std::min(MAXSTACK, std::max(2, bvh_max_stack(s->bvh_nodes, s->num_bvh_nodes)));
+        // VAR_BVH_FAST pair layout (DevPair): walk the tree in the reference's visit order
+        // (push left, push right, pop -> right subtree first), numbering internal nodes (pairs)
+        // and leaves (4-slot triangle groups).  Any tree this layout cannot hold exactly -- a
+        // missing child, a node reached twice, a leaf of more than 4 triangles, more than 65535
+        // refs or a deeper tree than the stack -- keeps the node-array traversal.
+        {
+            const int nn = s->num_bvh_nodes;
+            std::vector<int> id(nn, -1);
+            std::vector<char> is_leaf(nn, 0);
+            std::vector<std::pair<int, int>> st{{0, 1}};
+            int P = 0, L = 0, height = 0;
+            bool ok = true;
+            std::vector<int> leaf_nodes;
+            while (!st.empty() && ok) {
+                const int n = st.back().first, d = st.back().second;
+                st.pop_back();
+                if (n < 0 || n >= nn || id[n] >= 0) { ok = false; break; }
+                height = std::max(height, d);
+                const pt_bvh_node& nd = s->bvh_nodes[n];
+                if (nd.triCount > 0 && nd.start >= 0) {
+                    if (nd.triCount > 4) ok = false;
+                    is_leaf[n] = 1;
+                    id[n] = L++;
+                    leaf_nodes.push_back(n);
+                } else {
+                    if (nd.left < 0 || nd.right < 0) { ok = false; break; }
+                    id[n] = P++;
+                    st.push_back({nd.left, d + 1});
+                    st.push_back({nd.right, d + 1});
+                }
+            }
+            ok = ok && (int64_t)P + L <= 65535 && height + 1 <= MAXSTACK && !(o.variant & VAR_BVH_NODES);
+            if (ok) {
+                auto ref = [&](int n) { return is_leaf[n] ? P + id[n] : id[n]; };
+                pairs.resize(std::max(1, P));
+                for (int n = 0; n < nn; ++n) {
+                    if (id[n] < 0 || is_leaf[n]) continue;
+                    const pt_bvh_node& nd = s->bvh_nodes[n];
+                    DevPair& pr = pairs[id[n]];
+                    const int kids[2] = {nd.left, nd.right};
+                    float4* lo[2] = {&pr.l_lo, &pr.r_lo};
+                    float4* hi[2] = {&pr.l_hi, &pr.r_hi};
+                    for (int k = 0; k < 2; ++k) {
+                        const int c = kids[k];
+                        const int rf = ref(c);
+                        float frf;
+                        memcpy(&frf, &rf, 4);
+                        *lo[k] = make_float4(nodes[c].lo.x, nodes[c].lo.y, nodes[c].lo.z, frf);
+                        *hi[k] = make_float4(nodes[c].hi.x, nodes[c].hi.y, nodes[c].hi.z, node_aux[c].y);
+                    }
+                }
+                hot4.assign(4 * (size_t)L, DevTriHot{});
+                for (int k = 0; k < L; ++k) {
+                    const pt_bvh_node& nd = s->bvh_nodes[leaf_nodes[k]];
+                    for (int i = 0; i < nd.triCount; ++i) hot4[4 * (size_t)k + i] = hot[nd.start + i];
+                    const int cnt = nd.triCount;
+                    memcpy(&hot4[4 * (size_t)k].c.z, &cnt, 4);
+                }
+                pair_root_ref = ref(0);
+                pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
+                pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
+                pair_count = P;
+                g.stack_depth = std::max(g.stack_depth, std::min(MAXSTACK, height + 1));
+            }
+        }
         g.bvh_lds = (size_t)g.stack_depth * BLOCK * sizeof(int);
     }
     for (int i = 0; i < s->num_geoms; ++i)
         if (s->geoms[i].materialid >= std::max(1, s->num_materials))
             return fail(PT_E_INVALID, "geom %d material %d out of range", i, s->geoms[i].materialid);
+    // VAR_BVH_SPLIT needs the pair layout, the fast traversal and an LDS geom table
+    g.split = g.has_bvh && !pairs.empty() && o.pipeline == PT_PIPELINE_FUSED && (o.variant & VAR_BVH_SPLIT) &&
+              (o.variant & VAR_BVH_FAST) && (o.variant & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) &&
+              s->num_geoms <= LDS_GEOMS;
+    const int nb = nblocks(std::max(1, g.local_pixels * g.batch));
+    // output segment s receives the survivors of the chunks c = s (mod NSEG): of k_bounce's, and
+    // in split mode also of k_bvh_bounce's (its chunks of the queue) -- twice the room then
+    g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK * (g.split ? 2 : 1);
+    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels * g.batch);
+    g.capacity = ((g.capacity + STILE - 1) / STILE) * STILE;   // tile-padded: kernels may read a whole tile
 
     RC(dalloc(&g.d_geoms, geoms.size()));
     RC(dalloc(&g.d_mats, mats.size()));
@@ -1265,9 +1455,22 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         RC(upload(g.d_nodes, nodes.data(), nodes.size()));
         RC(upload(g.d_hot, hot.data(), hot.size()));
         RC(upload(g.d_cold, cold.data(), cold.size()));
+        if (!pairs.empty()) {
+            RC(dalloc(&g.d_pairs, pairs.size()));
+            RC(upload(g.d_pairs, pairs.data(), pairs.size()));
+            RC(dalloc(&g.d_hot4, hot4.size()));
+            RC(upload(g.d_hot4, hot4.data(), hot4.size()));
+        }
     }
     for (int i = 0; i < 2; ++i)
         for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
+    if (g.split) {
+        const size_t qn = (size_t)g.local_pixels * g.batch;
+        RC(dalloc(&g.queue.A, qn));
+        RC(dalloc(&g.queue.B, qn));
+        RC(dalloc(&g.queue.C, qn));
+        RC(dalloc(&g.queue.D, qn));
+    }
     RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
     RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
@@ -1329,6 +1532,16 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.texels = g.d_texels;
     sc.texinfo = g.d_texinfo;
     sc.num_textures = num_tex;
+    sc.pairs = g.d_pairs;
+    sc.hot4 = g.d_hot4;
+    sc.num_pairs = pair_count;
+    sc.root_ref = pair_root_ref;
+    sc.root_lo = pair_root_lo;
+    sc.root_hi = pair_root_hi;
+    // node_aux's c = 64 2^-24 sx^2 / 1e-5, stored x 1.01, and cE = c x extent x 1.01: the same
+    // bounds from s = sx on the device, rounded up
+    sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
+    sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
     g.inited = true;
     HIPCHK(hipDeviceSynchronize());
     return PT_OK;

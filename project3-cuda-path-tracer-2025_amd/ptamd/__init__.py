@@ -325,7 +325,7 @@ class PathTracer:
                 "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms}
 
     SECTIONS = ["load", "cull", "exact", "finish", "shade", "store", "n_exact", "n_cand", "n_iters", "n_waves",
-                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch"]
+                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers"]
 
     def section_counters(self, reset: bool = True) -> dict:
         """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""

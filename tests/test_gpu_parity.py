@@ -88,7 +88,8 @@ def _oracle_isects(oracle, a, paths):
 
 @pytest.mark.parametrize("name,variant", [("cornell", 10), ("cornell_obj_bnnuy", 10), ("cornell_obj_khaslana", 10),
                                           ("synthetic_textured_bump", 10), ("cornell_obj_bnnuy", 26),
-                                          ("cornell_obj_khaslana", 26), ("synthetic_textured_bump", 26)])
+                                          ("cornell_obj_khaslana", 26), ("synthetic_textured_bump", 26),
+                                          ("cornell_obj_bnnuy", 90), ("cornell_obj_khaslana", 90)])
 def test_intersect_bitexact(name, variant, oracle, ptamd):
     a, b = _oracle_pair(oracle, ptamd, name, (96, 96))      # wavefront capacity >= 9216 paths
     tr = ptamd.PathTracer(b, variant=variant)
@@ -190,6 +191,12 @@ FRAME_CASES = [
     ("cornell_obj_bnnuy", (64, 64), None, {"variant": 26}),             # fast BVH traversal
     ("cornell_obj_bnnuy", (64, 64), None, {"variant": 18, "pipeline": 1}),
     ("cornell_obj_khaslana", (48, 48), 12, {"variant": 26}),
+    ("cornell_obj_bnnuy", (64, 64), None, {"variant": 90}),             # fast BVH on the node array
+    ("cornell_obj_khaslana", (48, 48), 12, {"variant": 90, "pipeline": 1}),
+    ("cornell_obj_bnnuy", (64, 64), None, {"variant": 58}),             # split: traversal queue kernel
+    ("cornell_obj_khaslana", (48, 48), 12, {"variant": 58}),
+    ("synthetic_textured_bump", (48, 48), None, {"variant": 58}),
+    ("cornell_obj_phatphuck_texture_test", (48, 48), None, {"variant": 58}),
     ("synthetic_textured_bump", (48, 48), None, {"variant": 26}),
     ("synthetic_textured_bump", (64, 64), None, {"pipeline": 1}),
     ("synthetic_textured_bump", (48, 48), None, {"pipeline": 1, "material_sort": 1}),

@@ -42,6 +42,8 @@ def main():
            "live_lanes_per_wave": round(lanes / max(1, c["n_waves"]), 2),
            "bvh_nodes_per_ray": round(c["n_nodes"] / max(1, c["n_bvh_rays"]), 2),
            "bvh_tris_per_ray": round(c["n_tris"] / max(1, c["n_bvh_rays"]), 2),
+           "bvh_wave_iters_per_wave": round(c["n_bvh_witers"] / max(1, c["n_waves"]), 2),
+           "bvh_simt_efficiency": round(c["n_nodes"] / max(1, 64 * c["n_bvh_witers"]), 3),
            "aabb_decision_mismatches": c["n_aabb_mismatch"], "raw": c}
     print(json.dumps(out, indent=1))
     tr.free()
