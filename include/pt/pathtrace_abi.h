@@ -190,6 +190,7 @@ typedef struct pt_kernel_times {
     float compact_scan_ms;       /* staged: compaction count + scan kernels per frame (compact_ms = scatter) */
     int32_t passes;              /* wavefront passes the `frames` frames were traced in */
     float combine_ms;            /* k_combine (per-frame planes -> image) per frame */
+    float bvh_ms[64];            /* split BVH traversal (variant 32): k_bvh_bounce's part of bounce_ms[b] */
 } pt_kernel_times;
 /* Trace `count` frames with iterations first_iteration.. eagerly, every kernel launched with
  * hipExtLaunchKernel start/stop events (timestamps of that dispatch itself) and no host

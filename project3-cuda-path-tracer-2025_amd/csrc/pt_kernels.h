@@ -369,90 +369,124 @@ PT_DEV float cull_threshold(const SceneDev& sc, float entry, float s) {
 }
 PT_DEV uint32_t pack_ref(int ref, float T) { return ((uint32_t)ref << 16) | (__float_as_uint(T) >> 16); }
 
+// traversal state of one ray on the pair layout
+struct TravState {
+    f3 ro, rd, rr;
+    float t_limit, t_hit, bu, bv;
+    int btri, cur, sp;
+    bool exact;
+};
+PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_limit) {
+    st.ro = ro;
+    st.rd = rd;
+    st.exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
+                 rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);   // NaN / inf ray
+    st.rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+    st.t_limit = t_limit;
+    st.t_hit = FLT_MAX_;
+    st.bu = st.bv = 0.f;
+    st.btri = 0x7fffffff;
+    st.sp = 0;
+    float e0;
+    st.cur = (aabb_decide(sc.root_lo, sc.root_hi, ro, rd, st.rr, st.exact, e0) &&
+              !(t_limit < cull_threshold(sc, e0, sc.root_hi.w)))
+                 ? sc.root_ref
+                 : -1;
+}
+// one node expansion or one leaf; st.cur < 0 afterwards: the ray is finished
+template <bool COUNT = false>
+PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
+    const int P = sc.num_pairs;
+    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
+    const int cur = st.cur;
+    bool next = false;
+    if (cur < P) {
+        if (COUNT) n_nodes++;
+        const DevPair pr = sc.pairs[cur];
+        float el = 0.f, er = 0.f;
+        bool pl = aabb_decide(pr.l_lo, pr.l_hi, st.ro, st.rd, st.rr, st.exact, el);
+        bool pb = aabb_decide(pr.r_lo, pr.r_hi, st.ro, st.rd, st.rr, st.exact, er);
+        const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
+        const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
+        pl = pl && !(t_best < Tl);
+        pb = pb && !(t_best < Tr);
+        const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
+        if (pl && pb) {
+            const bool lfirst = el <= er;
+            st.cur = lfirst ? rl : rrf;
+            const int far = lfirst ? rrf : rl;
+            const float Tf = lfirst ? Tr : Tl;
+            if (st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
+            next = true;
+        } else if (pl | pb) {
+            st.cur = pl ? rl : rrf;
+            next = true;
+        }
+    } else {
+        // all four slots, loads issued together: unused slots hold a degenerate (all-zero)
+        // triangle, which intersectTriangle rejects (det = 0) or reports with t = NaN (NaN
+        // ray), and `t > 0` never accepts
+        const int base = 4 * (cur - P);
+        DevTriHot tq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tq[i] = sc.hot4[base + i];
+        if (COUNT) { n_nodes++; n_tris += __float_as_int(tq[0].c.z); }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const DevTriHot& th = tq[i];
+            const f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+            const f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+            const f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+            float t, u, v;
+            if (tri_test(st.ro, st.rd, v0, v1, v2, t, u, v) && t > 0.0f &&
+                (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
+                st.t_hit = t;
+                st.bu = u;
+                st.bv = v;
+                st.btri = base + i;
+            }
+        }
+    }
+    if (!next) {
+        const float tb = __builtin_fminf(st.t_hit, st.t_limit);
+        st.cur = -1;
+        while (st.sp > 0) {
+            const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
+            if (!(tb < __uint_as_float(w << 16))) {
+                st.cur = (int)(w >> 16);
+                break;
+            }
+        }
+    }
+}
+// result of a finished traversal: t (-1: no triangle), u, v, hot4 slot (-1)
+PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
+    if (st.t_hit == FLT_MAX_) {
+        btri = -1;
+        return -1.f;
+    }
+    bu = st.bu;
+    bv = st.bv;
+    btri = st.btri;
+    return st.t_hit;
+}
+
 template <bool COUNT = false>
 PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
                                  int& btri) {
     int n_nodes = 0, n_tris = 0;
-    const bool exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
-                         rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);   // NaN / inf ray
-    const f3 rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-    float t_hit = FLT_MAX_;
-    btri = 0x7fffffff;
-    float e0;
-    if (!aabb_decide(sc.root_lo, sc.root_hi, ro, rd, rr, exact, e0)) return -1.f;
-    if (t_limit < cull_threshold(sc, e0, sc.root_hi.w)) return -1.f;
-    const int P = sc.num_pairs;
-    int cur = sc.root_ref;
-    int sp = 0;
-    while (true) {
+    TravState st;
+    trav_begin(sc, st, ro, rd, t_limit);
+    while (st.cur >= 0) {
         if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
-        const float t_best = __builtin_fminf(t_hit, t_limit);
-        bool next = false;
-        if (cur < P) {
-            if (COUNT) n_nodes++;
-            const DevPair pr = sc.pairs[cur];
-            float el = 0.f, er = 0.f;
-            bool pl = aabb_decide(pr.l_lo, pr.l_hi, ro, rd, rr, exact, el);
-            bool pb = aabb_decide(pr.r_lo, pr.r_hi, ro, rd, rr, exact, er);
-            const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
-            const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
-            pl = pl && !(t_best < Tl);
-            pb = pb && !(t_best < Tr);
-            const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
-            if (pl && pb) {
-                const bool lfirst = el <= er;
-                cur = lfirst ? rl : rrf;
-                const int far = lfirst ? rrf : rl;
-                const float Tf = lfirst ? Tr : Tl;
-                if (sp < sc.stack_depth) stack[(sp++) * BLOCK] = (int)pack_ref(far, Tf);
-                next = true;
-            } else if (pl | pb) {
-                cur = pl ? rl : rrf;
-                next = true;
-            }
-        } else {
-            const int base = 4 * (cur - P);
-            const DevTriHot t0 = sc.hot4[base];
-            const int cnt = __float_as_int(t0.c.z);
-            if (COUNT) { n_nodes++; n_tris += cnt; }
-            for (int i = 0; i < cnt; ++i) {
-                const DevTriHot th = i == 0 ? t0 : sc.hot4[base + i];
-                const f3 v0 = mk(th.a.x, th.a.y, th.a.z);
-                const f3 v1 = mk(th.a.w, th.b.x, th.b.y);
-                const f3 v2 = mk(th.b.z, th.b.w, th.c.x);
-                float t, u, v;
-                if (tri_test(ro, rd, v0, v1, v2, t, u, v) && t > 0.0f &&
-                    (t < t_hit || (t == t_hit && base + i < btri))) {
-                    t_hit = t;
-                    bu = u;
-                    bv = v;
-                    btri = base + i;
-                }
-            }
-        }
-        if (!next) {
-            const float tb = __builtin_fminf(t_hit, t_limit);
-            cur = -1;
-            while (sp > 0) {
-                const uint32_t w = (uint32_t)stack[(--sp) * BLOCK];
-                if (!(tb < __uint_as_float(w << 16))) {
-                    cur = (int)(w >> 16);
-                    break;
-                }
-            }
-            if (cur < 0) break;
-        }
+        trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
     }
     if (COUNT) {
         sec_add_lanes(SEC_N_NODES, n_nodes);
         sec_add_lanes(SEC_N_TRIS, n_tris);
         sec_add_lanes(SEC_N_BVH_RAYS, 1);
     }
-    if (t_hit == FLT_MAX_) {
-        btri = -1;
-        return -1.f;
-    }
-    return t_hit;
+    return trav_result(st, bu, bv, btri);
 }
 
 // VAR_BVH_SPLIT: does bvh_intersect_pairs do anything for this ray beyond its root test?  The
@@ -503,9 +537,10 @@ PT_DEV bool cull_geom(const DevGeom& g, const CullRay& c, float t_min) {
 
 // winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
 // miss / facing conventions of pathtrace.cu:397-446
-template <bool HAS_BVH, bool BVH_FAST = false, bool COUNT = false>
-PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
-                      f3 seed, bool traverse = true) {
+// the winner's hit record from the primitive winner (t_min, win, seed) and the mesh result
+// (tb, u, v, slot of the winning triangle in `hot`; tb <= 0: none), pathtrace.cu:397-446
+PT_DEV Hit make_hit(const SceneDev& sc, const DevGeom* geoms, f3 rd, float t_min, int win, f3 seed, float tb, float u,
+                    float v, int tri, const DevTriHot* hot) {
     Hit h;
     h.tri = -1;
     h.u = 0.f;
@@ -519,37 +554,27 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
         hit_index = g.materialid;
         mat = g.materialid;
     }
-    if (HAS_BVH) {
-        if (traverse && sc.use_bvh && sc.num_nodes > 0) {
-            float u, v;
-            int tri;
-            const bool pairs = BVH_FAST && sc.pairs != nullptr;
-            float tb = pairs ? bvh_intersect_pairs<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
-                     : BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
-                                : bvh_intersect<COUNT>(sc, ro, rd, stack, u, v, tri);
-            if (tb > 0.0f && tb < t_min) {
-                t_min = tb;
-                hit_index = -2;
-                DevTriHot th = (pairs ? sc.hot4 : sc.hot)[tri];   // traversal returns the slot
-                int tri_index = __float_as_int(th.c.y);
-                const DevTriCold& cd = sc.cold[tri_index];
-                mat = cd.materialID;
-                h.tri = tri_index;
-                h.u = u;
-                h.v = v;
-                f3 n0 = mk(cd.n0[0], cd.n0[1], cd.n0[2]);
-                f3 n1 = mk(cd.n1[0], cd.n1[1], cd.n1[2]);
-                f3 n2 = mk(cd.n2[0], cd.n2[1], cd.n2[2]);
-                if (length(n0) < 1e-6f || length(n1) < 1e-6f || length(n2) < 1e-6f) {
-                    f3 v0 = mk(th.a.x, th.a.y, th.a.z);
-                    f3 v1 = mk(th.a.w, th.b.x, th.b.y);
-                    f3 v2 = mk(th.b.z, th.b.w, th.c.x);
-                    normal = normalize(cross(v1 - v0, v2 - v0));
-                } else {
-                    float w0 = 1.0f - u - v;
-                    normal = normalize((w0 * n0 + u * n1) + v * n2);
-                }
-            }
+    if (tb > 0.0f && tb < t_min) {
+        t_min = tb;
+        hit_index = -2;
+        DevTriHot th = hot[tri];
+        int tri_index = __float_as_int(th.c.y);
+        const DevTriCold& cd = sc.cold[tri_index];
+        mat = cd.materialID;
+        h.tri = tri_index;
+        h.u = u;
+        h.v = v;
+        f3 n0 = mk(cd.n0[0], cd.n0[1], cd.n0[2]);
+        f3 n1 = mk(cd.n1[0], cd.n1[1], cd.n1[2]);
+        f3 n2 = mk(cd.n2[0], cd.n2[1], cd.n2[2]);
+        if (length(n0) < 1e-6f || length(n1) < 1e-6f || length(n2) < 1e-6f) {
+            f3 v0 = mk(th.a.x, th.a.y, th.a.z);
+            f3 v1 = mk(th.a.w, th.b.x, th.b.y);
+            f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+            normal = normalize(cross(v1 - v0, v2 - v0));
+        } else {
+            float w0 = 1.0f - u - v;
+            normal = normalize((w0 * n0 + u * n1) + v * n2);
         }
     }
     if (hit_index == -1) {
@@ -563,6 +588,21 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
     h.n = normal;
     h.mat = mat;
     return h;
+}
+
+// winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
+// miss / facing conventions of pathtrace.cu:397-446
+template <bool HAS_BVH, bool BVH_FAST = false, bool COUNT = false>
+PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
+                      f3 seed, bool traverse = true) {
+    float tb = -1.f, u = 0.f, v = 0.f;
+    int tri = -1;
+    const bool pairs = BVH_FAST && sc.pairs != nullptr;
+    if (HAS_BVH && traverse && sc.use_bvh && sc.num_nodes > 0)
+        tb = pairs ? bvh_intersect_pairs<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
+           : BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
+                      : bvh_intersect<COUNT>(sc, ro, rd, stack, u, v, tri);
+    return make_hit(sc, geoms, rd, t_min, win, seed, tb, u, v, tri, pairs ? sc.hot4 : sc.hot);
 }
 
 // computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     constexpr bool REDIST = (VAR & VAR_WAVE_REDIST) != 0;
     constexpr bool BVH_FAST = (VAR & VAR_BVH_FAST) != 0;
     // split: the launcher guarantees the pair layout and an LDS geom table (queue or redist)
-    constexpr bool SPLIT = HAS_BVH && BVH_FAST && (VAR & VAR_BVH_SPLIT) && (QUEUE || REDIST) && !TIMING;
+    constexpr bool SPLIT = HAS_BVH && BVH_FAST && (VAR & VAR_BVH_SPLIT) && (QUEUE || REDIST);
     uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
     const bool lds_geoms = (QUEUE || REDIST) && sc.num_geoms <= LDS_GEOMS;
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     if (REDIST && lds_geoms) {                     // wave-cooperative: every lane takes part
         wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
     } else if (SPLIT && live) {
-        prim_intersect_q(sc, s_geoms, p.o, p.d, qt, qw, qs);
+        prim_intersect_q<TIMING>(sc, s_geoms, p.o, p.d, qt, qw, qs);
     }
     if (live) {
         if (SPLIT) {
@@ -314,6 +314,7 @@ __global__ __launch_bounds__(BLOCK) void k_bvh_bounce(SceneDev sc, QueueBuf q, P
     const int n = ctl->qcnt[bounce][0];
     const int block_start = blockIdx.x * BLOCK;
     if (block_start >= n) return;
+    int* s_stack = reinterpret_cast<int*>(s_dyn);
     const int iter = ctl->iter;
     const int batch = ctl->batch;
     const int tid = threadIdx.x;
@@ -331,8 +332,8 @@ __global__ __launch_bounds__(BLOCK) void k_bvh_bounce(SceneDev sc, QueueBuf q, P
         const int cw = __float_as_int(c.w);
         p.slot = cw & 255;
         const int win = (cw >> 8) - 1;
-        const Hit h = finish_hit<true, true>(sc, sc.geoms, p.o, p.d, reinterpret_cast<int*>(s_dyn) + tid, d.x, win,
-                                             mk(d.y, d.z, d.w));
+        const Hit h = finish_hit<true, true, (VAR & VAR_SECTION_TIMING) != 0>(sc, sc.geoms, p.o, p.d, s_stack + tid,
+                                                                             d.x, win, mk(d.y, d.z, d.w));
         shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     const bool surv = active && p.rb > 0;
@@ -758,7 +759,8 @@ PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path
 // execution time, independent of how far ahead of the GPU the host is.
 struct ProfRec {
     int kind;            // -1 frame begin, 0 camera, 1 intersect, 2 shade, 3 compact scatter,
-                         // 4 material sort, 5 compact count+scan, 100+b fused bounce b
+                         // 4 material sort, 5 compact count+scan, 100+b fused bounce b,
+                         // 200+b its split BVH traversal kernel
     hipEvent_t start, stop;
 };
 std::vector<ProfRec>* g_prof = nullptr;
@@ -799,7 +801,7 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + redist_lds, g.sc, in, out,
            g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
     if (SPLIT)
-        launch(100 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds, g.sc, g.queue, out, g.d_ctl, g.d_image, b,
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds, g.sc, g.queue, out, g.d_ctl, g.d_image, b,
                g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
@@ -815,6 +817,7 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 22: launch_bounce_t<FIRST, HAS_BVH, 22>(grid, in, out, b); break;
         case 50: launch_bounce_t<FIRST, HAS_BVH, 50>(grid, in, out, b); break;
         case 58: launch_bounce_t<FIRST, HAS_BVH, 58>(grid, in, out, b); break;
+        case 54: launch_bounce_t<FIRST, HAS_BVH, 54>(grid, in, out, b); break;   // split + section counters
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -1392,6 +1395,17 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                     st.push_back({nd.right, d + 1});
                 }
             }
+            if (ok) {   // internal refs breadth-first: the top levels share a few cache lines
+                std::vector<int> fifo{0};
+                int k = 0;
+                for (size_t h = 0; h < fifo.size(); ++h) {
+                    const int n = fifo[h];
+                    if (is_leaf[n]) continue;
+                    id[n] = k++;
+                    fifo.push_back(s->bvh_nodes[n].left);
+                    fifo.push_back(s->bvh_nodes[n].right);
+                }
+            }
             ok = ok && (int64_t)P + L <= 65535 && height + 1 <= MAXSTACK && !(o.variant & VAR_BVH_NODES);
             if (ok) {
                 auto ref = [&](int n) { return is_leaf[n] ? P + id[n] : id[n]; };
@@ -1883,7 +1897,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     (void)hipEventRecord(e1, g.stream);
     hipError_t se = hipStreamSynchronize(g.stream);
     const int passes = (int)pass_start.size();
-    double bounce_ms[MAXB] = {0};
+    double bounce_ms[MAXB] = {0}, bvh_ms[MAXB] = {0};
     double compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0, scan_ms = 0, comb_ms = 0;
     float frame_ms = 0;
     if (rc == PT_OK && se == hipSuccess) {
@@ -1895,7 +1909,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, rec[i].start, rec[i].stop);
                 int k = rec[i].kind;
-                if (k >= 100) bounce_ms[k - 100] += ms;
+                if (k >= 200) { bounce_ms[k - 200] += ms; bvh_ms[k - 200] += ms; }
+                else if (k >= 100) bounce_ms[k - 100] += ms;
                 else if (k == 0) cam_ms += ms;
                 else if (k == 1) isect_ms += ms;
                 else if (k == 2) shade_ms += ms;
@@ -1917,7 +1932,10 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     out->frames = count;
     out->passes = passes;
     out->frame_ms = frame_ms / count;
-    for (int b = 0; b < MAXB; ++b) out->bounce_ms[b] = (float)(bounce_ms[b] / passes);
+    for (int b = 0; b < MAXB; ++b) {
+        out->bounce_ms[b] = (float)(bounce_ms[b] / passes);
+        out->bvh_ms[b] = (float)(bvh_ms[b] / passes);
+    }
     out->combine_ms = (float)(comb_ms / count);
     out->compact_ms = (float)(compact_ms / count);
     out->intersect_ms = (float)(isect_ms / count);

@@ -81,7 +81,7 @@ class _KernelTimes(ctypes.Structure):
                 ("compact_ms", ctypes.c_float), ("intersect_ms", ctypes.c_float), ("shade_ms", ctypes.c_float),
                 ("camera_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("compact_bytes", ctypes.c_int64),
                 ("frame_bytes", ctypes.c_int64), ("compact_scan_ms", ctypes.c_float), ("passes", ctypes.c_int32),
-                ("combine_ms", ctypes.c_float)]
+                ("combine_ms", ctypes.c_float), ("bvh_ms", ctypes.c_float * 64)]
 
 
 # every symbol the C-ABI header declares (tests check the library exports all of them)
@@ -321,6 +321,7 @@ class PathTracer:
         self.iteration = first_iteration + count - 1
         return {"frames": t.frames, "passes": t.passes, "frame_ms": t.frame_ms, "combine_ms": t.combine_ms,
                 "bounce_ms": [t.bounce_ms[i] for i in range(max(1, self.trace_depth))],
+                "bvh_ms": [t.bvh_ms[i] for i in range(max(1, self.trace_depth))],
                 "compact_ms": t.compact_ms, "intersect_ms": t.intersect_ms, "shade_ms": t.shade_ms,
                 "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms}
 
