@@ -58,6 +58,24 @@ PT_DEV f3 cross(f3 x, f3 y) {
 PT_DEV float length(f3 v) { return __builtin_sqrtf(dot(v, v)); }
 // normalize = x * (1 / sqrt(dot(x, x)))  (func_geometric.inl:158, func_exponential.inl:150-153)
 PT_DEV f3 normalize(f3 v) { return v * (1.0f / __builtin_sqrtf(dot(v, v))); }
+// The same normalize, bit for bit, cheaper for a v that is already (nearly) unit length.  When
+// d = dot(v, v) lies within NU_ULPS floats of 1, both IEEE roundings (s = sqrt(d), then 1 / s)
+// follow from d's bits alone:
+//   d = 1 + k 2^-23 (0 <= k):  s = 1 + floor(k/2) 2^-23,  1/s = 1 - floor(k/2) 2^-23
+//   d = 1 - k 2^-24 (1 <= k):  s = 1 - ceil(k/2) 2^-24,   1/s = 1 + ceil(ceil(k/2)/2) 2^-23
+// (tests/test_unit_normalize.py checks every such d against IEEE sqrtf and division).  Any
+// other d, NaN included, takes the IEEE sequence.
+constexpr int NU_ULPS = 64;
+PT_DEV float inv_sqrt_near1_bits(int k) {   // k = bits(d) - bits(1.0f), |k| <= NU_ULPS
+    const int m = k >= 0 ? -2 * (k >> 1) : ((((1 - k) >> 1) + 1) >> 1);
+    return __int_as_float(0x3f800000 + m);
+}
+PT_DEV f3 normalize_unit(f3 v) {
+    const float d = dot(v, v);
+    const int k = (int)__float_as_uint(d) - 0x3f800000;
+    if (k >= -NU_ULPS && k <= NU_ULPS) return v * inv_sqrt_near1_bits(k);
+    return v * (1.0f / __builtin_sqrtf(d));
+}
 PT_DEV f3 reflect(f3 I, f3 N) { return I - (N * dot(N, I)) * 2.0f; }
 // glm 0.9.6 refract: NaN (not 0) on total internal reflection
 PT_DEV f3 refract(f3 I, f3 N, float eta) {
@@ -192,7 +210,7 @@ PT_DEV float u01(Rng& r) { return (float)(rng_next(r) - 1u) * 4.6566128730773925
 // primitives (intersections.cu)
 // ------------------------------------------------------------------------------------------
 // getPointOnRay, intersections.h:29-32
-PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize(d); }
+PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize_unit(d); }   // d: unit q.direction
 
 // boxIntersectionTest (intersections.cu:3-57) and sphereIntersectionTest (intersections.cu:
 // 59-109) as ONE routine: both start by taking the ray to object space (q.origin, normalized
@@ -363,7 +381,7 @@ PT_DEV f3 sample_diffuse(f3 albedo, f3 normal, f3& wiW, float& pdf, Rng& rng, in
     u01_pair(rng, arg_order, xi0, xi1);
     f3 wi = hemisphere_cosine(xi0, xi1);
     M3 ws = local_to_world(normal);
-    wiW = normalize(mul(ws, wi));
+    wiW = normalize_unit(mul(ws, wi));
     pdf = wi.z / PI;
     return albedo * INV_PI;
 }
@@ -373,7 +391,7 @@ PT_DEV f3 sample_spec_trans(f3 albedo, f3 normal, f3 wo, float IOR, f3& wiW) {
     bool entering = dot(wo, normal) < 0.0f;
     float eta = entering ? (1.0f / IOR) : IOR;
     f3 outNormal = entering ? normal : -normal;
-    wiW = refract(normalize(wo), normalize(outNormal), eta);
+    wiW = refract(normalize_unit(wo), normalize_unit(outNormal), eta);
     if (length(wiW) < BABY_EPSILON) {
         wiW = reflect(wo, normal);
         return mk(0.f, 0.f, 0.f);
@@ -478,7 +496,7 @@ PT_DEV f3 sample_microfacet(f3 albedo, f3 normal, f3 wo, float r, float metallic
     f3 wh_local = sample_wh(wo_local, r, rng, arg_order);
     if (wh_local.z < 0.0f) wh_local = -wh_local;
     f3 wi_local = reflect(-wo_local, wh_local);
-    wiW = normalize(mul(l2w, wi_local));
+    wiW = normalize_unit(mul(l2w, wi_local));
     float dotWO_WH = gmax(dot(wo_local, wh_local), 1e-6f);
     pdf = (tr_d(wh_local, r) * __builtin_fabsf(wh_local.z)) / (4.0f * dotWO_WH);
     return f_microfacet(albedo, wo_local, wi_local, r, metallic);
@@ -515,29 +533,29 @@ PT_DEV void scatter(PathReg& p, f3 intersect, f3 normal, const DevMaterial& m, f
     float pdf = 1.0f;
     if (m.hasRefractive > 0.0f && m.hasReflective > 0.0f) {          // Glass
         bsdf = sample_glass(mcolor, normal, p.d, m.ior, wiW, rng);
-        p.d = normalize(wiW);
+        p.d = normalize_unit(wiW);
         p.o = intersect + p.d * LARGER_EPSILON;
         p.c = p.c * bsdf;
     } else if (m.hasReflective > 0.0f) {                              // Mirror
         wiW = reflect(p.d, normal);
-        p.d = normalize(wiW);
+        p.d = normalize_unit(wiW);
         p.o = intersect + normal * BABY_EPSILON;
         p.c = p.c * mcolor;
     } else if (m.hasRefractive > 0.0f) {                              // Transmissive
         bsdf = sample_spec_trans(mcolor, normal, p.d, m.ior, wiW);
-        p.d = normalize(wiW);
+        p.d = normalize_unit(wiW);
         p.o = intersect + p.d * LARGER_EPSILON;
         p.c = p.c * bsdf;
     } else if (m.roughness >= 0.0f && m.metallic >= 0.0f) {           // Microfacet
-        f3 woW = -normalize(p.d);
+        f3 woW = -normalize_unit(p.d);
         bsdf = sample_cook_torrance(mcolor, normal, woW, m.roughness, m.metallic, wiW, pdf, rng, arg_order);
-        p.d = normalize(wiW);
+        p.d = normalize_unit(wiW);
         p.o = intersect + p.d * LARGER_EPSILON;
         float cosTheta = gmax(0.0f, dot(normal, wiW));
         if (pdf > 0.0f) p.c = p.c * ((bsdf * cosTheta) / pdf);
     } else {                                                          // Diffuse
         bsdf = sample_diffuse(mcolor, normal, wiW, pdf, rng, arg_order);
-        p.d = normalize(wiW);
+        p.d = normalize_unit(wiW);
         p.o = intersect + normal * BABY_EPSILON;
         float cosTheta = gmax(0.0f, dot(normal, wiW));
         p.c = p.c * ((bsdf * cosTheta) / pdf);

@@ -426,17 +426,22 @@ PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_node
         // all four slots, loads issued together: unused slots hold a degenerate (all-zero)
         // triangle, which intersectTriangle rejects (det = 0) or reports with t = NaN (NaN
         // ray), and `t > 0` never accepts
+        // (positions only: the third record word is read as one float, v2.z)
         const int base = 4 * (cur - P);
-        DevTriHot tq[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) tq[i] = sc.hot4[base + i];
-        if (COUNT) { n_nodes++; n_tris += __float_as_int(tq[0].c.z); }
+        float4 ta[4], tb[4];
+        float tc[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const DevTriHot& th = tq[i];
-            const f3 v0 = mk(th.a.x, th.a.y, th.a.z);
-            const f3 v1 = mk(th.a.w, th.b.x, th.b.y);
-            const f3 v2 = mk(th.b.z, th.b.w, th.c.x);
+            ta[i] = sc.hot4[base + i].a;
+            tb[i] = sc.hot4[base + i].b;
+            tc[i] = sc.hot4[base + i].c.x;
+        }
+        if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f3 v0 = mk(ta[i].x, ta[i].y, ta[i].z);
+            const f3 v1 = mk(ta[i].w, tb[i].x, tb[i].y);
+            const f3 v2 = mk(tb[i].z, tb[i].w, tc[i]);
             float t, u, v;
             if (tri_test(st.ro, st.rd, v0, v1, v2, t, u, v) && t > 0.0f &&
                 (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {

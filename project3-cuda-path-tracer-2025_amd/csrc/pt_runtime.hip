@@ -323,17 +323,24 @@ __global__ __launch_bounds__(BLOCK) void k_bvh_bounce(SceneDev sc, QueueBuf q, P
     PathReg p;
     p.rb = 0;
     if (active) {
-        const float4 a = q.A[gid], b = q.B[gid], c = q.C[gid], d = q.D[gid];
+        // traversal needs only the ray and its primitive t; the rest of the queue entry is
+        // fetched afterwards (fewer registers live across the traversal loop -> occupancy)
+        const float4 a = q.A[gid], b = q.B[gid];
+        const float t_prim = q.D[gid].x;
         p.o = mk(a.x, a.y, a.z);
-        p.pix = __float_as_int(a.w);
         p.d = mk(b.x, b.y, b.z);
-        p.rb = __float_as_int(b.w);
+        float u = 0.f, v = 0.f;
+        int tri = -1;
+        const float tb = bvh_intersect_pairs<(VAR & VAR_SECTION_TIMING) != 0>(sc, p.o, p.d, s_stack + tid, t_prim, u,
+                                                                             v, tri);
+        const float4 c = q.C[gid], d = q.D[gid];
+        p.pix = __float_as_int(q.A[gid].w);
+        p.rb = __float_as_int(q.B[gid].w);
         p.c = mk(c.x, c.y, c.z);
         const int cw = __float_as_int(c.w);
         p.slot = cw & 255;
         const int win = (cw >> 8) - 1;
-        const Hit h = finish_hit<true, true, (VAR & VAR_SECTION_TIMING) != 0>(sc, sc.geoms, p.o, p.d, s_stack + tid,
-                                                                             d.x, win, mk(d.y, d.z, d.w));
+        const Hit h = make_hit(sc, sc.geoms, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
         shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     const bool surv = active && p.rb > 0;
