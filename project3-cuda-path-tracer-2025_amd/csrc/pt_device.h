@@ -118,9 +118,24 @@ struct DevGeom {
     float box_hi[3];
     int32_t type;
     int32_t materialid;
-    int32_t _pad[4];
+    int32_t away_axis;  // cubes: object axis of the smallest scale for the pre-test's "away" drop
+                        // (see away_on_axis); -1: none (spheres, or matrices too large to bound)
+    int32_t _pad[3];
 };
 static_assert(sizeof(DevGeom) == 192, "DevGeom");
+
+// geom_test's cube early-out, on ONE object axis a, with geom_test's own arithmetic for qo[a]
+// and u[a] (xform row a).  True only when geom_test would return -1 through that early-out: the
+// object-space origin is outside slab a and the direction points away.  u[a]'s w term
+// (m[9 + a] * 0 = +-0) is left out: it cannot change a nonzero u[a], and `u > 0` / `u < 0` are
+// false for either zero.  geom_test also requires dot(u, u) < inf; the caller guarantees it
+// (|rd| components <= 1e3 and |inv| entries <= 1e12, checked on the host).
+PT_DEV bool away_on_axis(const DevGeom& g, int a, f3 ro, f3 rd) {
+    const float* m = g.inv;
+    const float qo = (m[a] * ro.x + m[3 + a] * ro.y) + (m[6 + a] * ro.z + m[9 + a] * 1.0f);
+    const float u = (m[a] * rd.x + m[3 + a] * rd.y) + m[6 + a] * rd.z;
+    return (qo > 0.5f && u > 0.0f) || (qo < -0.5f && u < 0.0f);
+}
 
 // 64-byte material: only what shading reads (sceneStructs.h:36-57)
 struct DevMaterial {

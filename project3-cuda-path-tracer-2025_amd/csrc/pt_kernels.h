@@ -746,9 +746,17 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
     CullRay cr;
     if (live) {
         cr = cull_ray(ro, rd);
+        // a ray leaving a surface keeps that surface's box as a candidate (its origin sits inside
+        // the margin), but geom_test's "away" early-out rejects it: drop such candidates here,
+        // with the same arithmetic, so they take no slot in the exchanged exact tests
+        const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
+                             __builtin_fabsf(rd.z) <= 1e3f;
 #pragma unroll 4
         for (int i = 0; i < sc.num_geoms; ++i)
-            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
+            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) {
+                const int a = sc.geoms[i].away_axis;
+                if (!(a >= 0 && bounded && away_on_axis(sc.geoms[i], a, ro, rd))) cand |= 1ull << i;
+            }
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;

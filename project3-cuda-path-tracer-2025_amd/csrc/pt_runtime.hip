@@ -1163,6 +1163,27 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             }
         d.type = gg.type;
         d.materialid = gg.materialid;
+        // away_on_axis pre-test: the object axis of smallest world scale (a wall's thin axis,
+        // the face a ray leaving it crosses); only when the inverse matrix is bounded so that
+        // dot(u, u) < inf is guaranteed for |rd| components <= 1e3
+        d.away_axis = -1;
+        if (gg.type == PT_CUBE) {
+            double big = 0.0;
+            for (int c = 0; c < 4; ++c)
+                for (int r = 0; r < 3; ++r) big = std::max(big, std::fabs((double)gg.inverseTransform.m[c][r]));
+            if (big <= 1e12) {
+                double best = 1e300;
+                for (int a = 0; a < 3; ++a) {
+                    const double len = std::sqrt((double)gg.transform.m[a][0] * gg.transform.m[a][0] +
+                                                 (double)gg.transform.m[a][1] * gg.transform.m[a][1] +
+                                                 (double)gg.transform.m[a][2] * gg.transform.m[a][2]);
+                    if (len < best) {
+                        best = len;
+                        d.away_axis = a;
+                    }
+                }
+            }
+        }
     }
     // conservative world boxes for cull_geom: the transformed unit cube (contains the radius-0.5
     // sphere too), grown by a margin far above every rounding the exact test can make (1e-3 of
