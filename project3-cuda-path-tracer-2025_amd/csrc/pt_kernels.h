@@ -639,18 +639,74 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
 // and re-checks the cull against its current t_min before the exact test.  The wave executes
 // max-over-lanes(candidates) exact tests instead of one per geom any lane needs.
 // `lgeoms`: the block's LDS copy of the geom table (the caller's job; sc.num_geoms <= 64).
-template <bool TIMING = false>
+// NEAR_FIRST (camera rays: neighbouring lanes share their nearest candidate, so the first test
+// is wave-coherent): each lane tests its candidate of smallest conservative entry distance
+// first; the rest, in index order, are then mostly re-culled as certainly farther.  Tested out
+// of index order, the first-minimum rule becomes "smaller t, or equal t and smaller index".
+PT_DEV float cull_entry(const DevGeom& g, const CullRay& c) {   // +inf: certain miss
+    const float a0 = __builtin_fmaf(g.box_lo[0], c.id.x, -c.rid.x), b0 = __builtin_fmaf(g.box_hi[0], c.id.x, -c.rid.x);
+    const float a1 = __builtin_fmaf(g.box_lo[1], c.id.y, -c.rid.y), b1 = __builtin_fmaf(g.box_hi[1], c.id.y, -c.rid.y);
+    const float a2 = __builtin_fmaf(g.box_lo[2], c.id.z, -c.rid.z), b2 = __builtin_fmaf(g.box_hi[2], c.id.z, -c.rid.z);
+    const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                     __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
+    const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                     __builtin_fmaxf(a2, b2));
+    return (t1 >= t0) ? t0 : __builtin_inff();
+}
+template <bool TIMING = false, bool NEAR_FIRST = false>
 PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, float& t_min, int& win,
                              f3& seed) {
     uint64_t tc0 = TIMING ? sec_clock() : 0;
     const CullRay cr = cull_ray(ro, rd);
     uint64_t cand = 0;
-#pragma unroll 4
-    for (int i = 0; i < sc.num_geoms; ++i)
-        if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
     t_min = FLT_MAX_;
     win = -1;
     seed = mk(0.f, 0.f, 0.f);
+    if (NEAR_FIRST) {
+        int first = -1;
+        float best = __builtin_inff();
+#pragma unroll 4
+        for (int i = 0; i < sc.num_geoms; ++i) {
+            const float e = cull_entry(sc.geoms[i], cr);
+            if (e != __builtin_inff()) {
+                cand |= 1ull << i;
+                if (e < best) {
+                    best = e;
+                    first = i;
+                }
+            }
+        }
+        if (first >= 0) {
+            cand &= ~(1ull << first);
+            f3 s;
+            const float t = geom_test(lgeoms[first], ro, rd, s);
+            if (t > 0.0f && t_min > t) {
+                t_min = t;
+                win = first;
+                seed = s;
+            }
+        }
+        while (__any(cand != 0)) {
+            if (cand != 0) {
+                const int i = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const DevGeom& g = lgeoms[i];
+                if (!cull_geom(g, cr, t_min)) {
+                    f3 s;
+                    const float t = geom_test(g, ro, rd, s);
+                    if (t > 0.0f && (t < t_min || (t == t_min && win >= 0 && i < win))) {
+                        t_min = t;
+                        win = i;
+                        seed = s;
+                    }
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll 4
+    for (int i = 0; i < sc.num_geoms; ++i)
+        if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) cand |= 1ull << i;
     int n_exact = 0, n_iters = 0;
     uint64_t tc1 = 0;
     if (TIMING) {
@@ -682,12 +738,12 @@ PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
         sec_add(SEC_N_ITERS, (uint64_t)n_iters);
     }
 }
-template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false>
+template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false, bool NEAR_FIRST = false>
 PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
     float t_min;
     int win;
     f3 seed;
-    prim_intersect_q<TIMING>(sc, lgeoms, ro, rd, t_min, win, seed);
+    prim_intersect_q<TIMING, NEAR_FIRST && !TIMING>(sc, lgeoms, ro, rd, t_min, win, seed);
     if (TIMING) {
         const uint64_t tc2 = sec_clock();
         Hit h = finish_hit<HAS_BVH, BVH_FAST, true>(sc, lgeoms, ro, rd, stack, t_min, win, seed);

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     if (REDIST && lds_geoms) {                     // wave-cooperative: every lane takes part
         wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
     } else if (SPLIT && live) {
-        prim_intersect_q<TIMING>(sc, s_geoms, p.o, p.d, qt, qw, qs);
+        prim_intersect_q<TIMING, FIRST && !TIMING>(sc, s_geoms, p.o, p.d, qt, qw, qs);
     }
     if (live) {
         if (SPLIT) {
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         } else if (REDIST && lds_geoms) {
             h = finish_hit<HAS_BVH, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else {
-            h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid)
+            h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST, FIRST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
         }
         if (!queued) {
