@@ -124,6 +124,9 @@ int32_t pt_trace(pt_uchar4* pbo_device, int32_t frame, int32_t iteration, float*
 /* Trace `count` frames with iterations first_iteration .. first_iteration+count-1, image stays
  * in HBM (no host copy, no PBO).  The throughput path used by bench.py. */
 int32_t pt_trace_frames(int32_t first_iteration, int32_t count);
+/* Capture (hipGraph) every pass size a later pt_trace_frames(., count) replays, so that call
+ * launches only.  Optional: pt_trace_frames captures on first use. */
+int32_t pt_prepare_frames(int32_t count);
 
 /* Block until all queued work finished. */
 int32_t pt_synchronize(void);

@@ -771,13 +771,22 @@ struct ProfRec {
     hipEvent_t start, stop;
 };
 std::vector<ProfRec>* g_prof = nullptr;
+std::vector<hipEvent_t> g_prof_pool;   // events created before the profiled run (no host-side
+size_t g_prof_next = 0;                // event creation between the timed launches)
+
+hipEvent_t prof_event() {
+    if (g_prof_next < g_prof_pool.size()) return g_prof_pool[g_prof_next++];
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    g_prof_pool.push_back(e);
+    g_prof_next = g_prof_pool.size();
+    return e;
+}
 
 template <class K, class... A>
 void launch(int kind, K kernel, dim3 grid, dim3 block, uint32_t lds, A... args) {
     if (g_prof) {
-        ProfRec r{kind, nullptr, nullptr};
-        (void)hipEventCreate(&r.start);
-        (void)hipEventCreate(&r.stop);
+        ProfRec r{kind, prof_event(), prof_event()};
         hipExtLaunchKernelGGL(kernel, grid, block, lds, g.stream, r.start, r.stop, 0, args...);
         g_prof->push_back(r);
     } else {
@@ -1631,6 +1640,17 @@ int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     return PT_OK;
 }
 
+int32_t pt_prepare_frames(int32_t count) {
+    RC(need_init());
+    if (count < 0) return fail(PT_E_INVALID, "bad count");
+    if (!g.opts.use_graph) return PT_OK;
+    // the pass sizes pt_trace_frames(., count) will replay: F, and the remainder
+    const int sizes[2] = {std::min(g.batch, count), count % g.batch};
+    for (int f : sizes)
+        if (f > 0 && !g.graph_exec[f]) RC(build_graph(f));
+    return PT_OK;
+}
+
 int32_t pt_synchronize(void) {
     RC(need_init());
     HIPCHK(hipStreamSynchronize(g.stream));
@@ -1910,6 +1930,16 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
+    {   // every kernel of every pass gets a start and a stop event, created up front
+        const int passes = (count + g.batch - 1) / g.batch;
+        const size_t need = 2 * (size_t)passes * (size_t)(4 * std::max(1, g.sc.trace_depth) + 8);
+        while (g_prof_pool.size() < need) {
+            hipEvent_t e = nullptr;
+            HIPCHK(hipEventCreate(&e));
+            g_prof_pool.push_back(e);
+        }
+        g_prof_next = 0;
+    }
     HIPCHK(hipEventRecord(e0, g.stream));
     g_prof = &rec;
     int rc = PT_OK;
@@ -1949,10 +1979,9 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
             }
         }
     }
-    for (auto& r : rec) {
-        (void)hipEventDestroy(r.start);
-        (void)hipEventDestroy(r.stop);
-    }
+    for (auto e : g_prof_pool) (void)hipEventDestroy(e);
+    g_prof_pool.clear();
+    g_prof_next = 0;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     RC(rc);

@@ -91,7 +91,7 @@ ABI_SYMBOLS = [
     "pt_get_frame_stats", "pt_reset_stats", "pt_set_camera", "pt_scene_load", "pt_scene_get_view", "pt_scene_get_info",
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
-    "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames",
+    "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
 ]
 
 
@@ -115,7 +115,7 @@ def _load():
         "pt_test_camera": (i32, [i32, vp, i64]), "pt_test_intersect": (i32, [vp, i64, vp]),
         "pt_test_shade": (i32, [i32, vp, vp, i64]), "pt_test_compact": (i32, [vp, i64, vp, vp]),
         "pt_test_sort": (i32, [vp, i64, vp]), "pt_test_rng": (i32, [vp, i64, i32, vp]),
-        "pt_test_pbo": (i32, [vp, i64, i32, vp]), "pt_profile_frames": (i32, [i32, i32, vp]),
+        "pt_test_pbo": (i32, [vp, i64, i32, vp]), "pt_profile_frames": (i32, [i32, i32, vp]), "pt_prepare_frames": (i32, [i32]),
         "pt_debug_section_counters": (i32, [vp, i32, i32]),
         "pt_texture_load": (i32, [ctypes.c_char_p, vp, vp, vp, i64]),
     }
@@ -285,6 +285,10 @@ class PathTracer:
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")
         self.iteration = first_iteration + count - 1
+
+    def prepare_frames(self, count: int):
+        """Capture the pass graphs trace_frames(., count) replays (keeps capture out of timing)."""
+        _check(lib.pt_prepare_frames(int(count)), "pt_prepare_frames")
 
     def synchronize(self):
         _check(lib.pt_synchronize(), "pt_synchronize")
