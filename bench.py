@@ -142,8 +142,13 @@ def main():
     if rank == 0:
         headline = (os.path.abspath(args.scene) == SCENE and not args.res and args.depth < 0 and not args.sort)
         name = os.path.basename(args.scene)
-        workload = (f"{name} {tr.width}x{tr.height} depth {depth}, stream compaction on, "
-                    f"sort {'on' if args.sort else 'off'}")
+        if args.sort and args.pipeline == "fused":
+            sort = ("material sort requested: the fused pipeline shades each path in registers right after "
+                    "its intersection, so there is nothing to sort (results are order-independent); "
+                    "--pipeline staged runs the sort")
+        else:
+            sort = f"sort {'on' if args.sort else 'off'}"
+        workload = f"{name} {tr.width}x{tr.height} depth {depth}, stream compaction on, {sort}"
         line = {
             "metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8" if headline
                       else f"Mpaths/s (rays x bounces / s), {workload}",

@@ -15,7 +15,7 @@ run() {   # run TAG ARGS...
 }
 run c2_fused   --steps 100 --warmup 10
 run c2_staged  --steps 100 --warmup 10 --pipeline staged
-run c3_fused   --steps 100 --warmup 10 --scene scenes/cornell_glass_test.json --sort
+run c3_fused   --steps 100 --warmup 10 --scene scenes/cornell_glass_test.json
 run c3_staged  --steps 100 --warmup 10 --scene scenes/cornell_glass_test.json --sort --pipeline staged
 run c4_fused   --steps 50 --warmup 8 --scene scenes/cornell_obj_bnnuy.json
 run c4_staged  --steps 50 --warmup 8 --scene scenes/cornell_obj_bnnuy.json --pipeline staged
