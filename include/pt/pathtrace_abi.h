@@ -84,8 +84,8 @@ typedef struct pt_options {
                                     full waves by a second kernel per bounce, 64: keep 16 on the
                                     reference node array instead of the paired-children layout);
                                     results are bit-identical for every value.  Default 2|8|16|32 */
-    int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..16;
-                                    0 = auto: ~5.2M paths in flight).  The image is bit-identical
+    int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..32;
+                                    0 = auto: ~21M paths in flight).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in
                                     per-frame planes that are added in frame order. */
 } pt_options;

@@ -708,8 +708,12 @@ int dalloc(T** p, size_t n) {
     return PT_OK;
 }
 
-constexpr int MAXF = 16;                    // frames per pass, upper bound
-constexpr int64_t AUTO_BATCH_PATHS = 5200000;   // 800x800: F = 8 (A/B: F=1 0.214, 2 0.161, 4 0.137, 8 0.129, 16 0.129 ms/frame)
+constexpr int MAXF = 32;                    // frames per pass, upper bound
+// auto F: up to ~21M paths at bounce 0 -> 800x800: F = 32, 1600x1600: F = 8.  A/B (ms/frame):
+// cornell 800^2 F = 8 0.0992, 16 0.0949 (0.0937), 32 0.0921; bunny 800^2 F = 8 0.685, 16 0.633;
+// khaslana 1600^2 F = 2 2.52, 4 1.95 (1.93), 8 1.66 (earlier kernels: F = 1 0.214, 2 0.161,
+// 4 0.137, 8 0.129).  ~4 GB of path buffers + 1.3 GB traversal queue at this size.
+constexpr int64_t AUTO_BATCH_PATHS = 21000000;
 
 struct State {
     bool inited = false;
@@ -1108,7 +1112,7 @@ int32_t pt_free(void) {
 }
 
 // frames per pass when pt_options.frames_per_pass == 0: enough paths in flight to fill the
-// chip in the late, mostly-terminated bounces (~5.2M paths at bounce 0), at most MAXF
+// chip in the late, mostly-terminated bounces (~21M paths at bounce 0), at most MAXF
 int auto_batch(int local_pixels) {
     int f = 1;
     while (f * 2 <= MAXF && (int64_t)local_pixels * f * 2 <= AUTO_BATCH_PATHS) f *= 2;
