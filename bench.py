@@ -222,8 +222,11 @@ def roofline(prof, st, args, depth, headline=True):
     avg_ms = sum(prof["bounce_ms"][:depth]) / depth
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     pmc = _pmc(name) if headline else {}     # the committed PMC pass is of the headline run
+    # measured HBM bytes per launch: the PMC run's bytes per frame x this run's frames per launch
+    traffic = (int(pmc["hbm_bytes_per_frame"] * args.steps / launches) if pmc.get("hbm_bytes_per_frame")
+               else pmc.get("hbm_bytes_per_launch"))
     line = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("hbm_bytes_per_launch"),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
             "duration_source": "HIP start/stop events per dispatch (hipExtLaunchKernel) over an eager replay of "
                                "K frames right after the timed region"}

@@ -39,8 +39,11 @@ def kernel_stats(path):
     return out
 
 
-def pmc(pmc_dir, prefix):
-    """mean counter value per dispatch, per kernel family, over every pass <prefix>p*/."""
+def pmc(pmc_dir, prefix, frames=0):
+    """mean counter value per dispatch, per kernel family, over every pass <prefix>p*/.  With
+    `frames` (frames each profiled run traced: warmup + timed + bench's profiling replay), also the
+    HBM bytes per FRAME: the sum over the run's dispatches / frames, independent of how the run's
+    frames were grouped into passes (bench.py scales it to its own launches)."""
     acc = defaultdict(lambda: defaultdict(list))
     for d in sorted(glob.glob(os.path.join(pmc_dir, prefix + "p*"))):
         if not os.path.isdir(d):
@@ -56,6 +59,10 @@ def pmc(pmc_dir, prefix):
         e["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             e["hbm_bytes_per_launch"] = int((2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024)
+            if frames:
+                tot = (2 * sum(cs["FETCH_SIZE"]) + sum(cs["WRITE_SIZE"])) * 1024
+                e["hbm_bytes_per_frame"] = int(tot / frames)
+                e["frames_per_run"] = frames
         res[fam] = e
     return res
 
@@ -65,6 +72,8 @@ def main():
     ap.add_argument("--round", default="r01")
     ap.add_argument("--stats", nargs=2, action="append", metavar=("DIR", "TAG"), default=[])
     ap.add_argument("--pmc", nargs=2, action="append", metavar=("DIR", "PREFIX"), default=[])
+    ap.add_argument("--pmc-frames", type=int, default=72,
+                    help="frames per profiled run (tools/pmc.sh: warmup 8 + steps 32 + bench's replay 32)")
     args = ap.parse_args()
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -78,7 +87,7 @@ def main():
             json.dump(digest, f, indent=1)
     traffic = {}
     for d, prefix in args.pmc:
-        for fam, e in pmc(d, prefix).items():
+        for fam, e in pmc(d, prefix, args.pmc_frames).items():
             traffic.setdefault(fam, {}).update(e)
             traffic[fam]["source"] = f"{prefix or 'default'} passes"
     if traffic:
