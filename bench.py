@@ -268,20 +268,30 @@ def pcie_copy_ms(tr):
 
 def cpu_baseline(budget_s):
     """The oracle (C port of the reference path: serial intersect/shade loops + cpu.cu's
-    compactWithScan) on this host, 1 thread, BASELINE configs[0] (cornell 400x400 depth 4)."""
+    compactWithScan) on this host, BASELINE configs[0] (cornell 400x400 depth 4): 1 thread for
+    `value`, and the same at this process's CPU share (OpenMP over paths) beside it."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     sc = O.load_scene(SCENE, res=(400, 400), depth=4)
-    r = O.Renderer(sc, O.options(num_threads=1))
-    segs, frames, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or frames < 2:
-        frames += 1
-        segs += int(np.maximum(r.trace(frames), 0).sum())
-    el = time.perf_counter() - t0
-    return {"value": round(segs / el / 1e6, 3), "unit": "Mpaths/s", "cores": 1, "kind": "port",
-            "sample": f"cornell.json 400x400 depth 4 (BASELINE configs[0]), {frames} frames in {el:.1f} s, "
-                      f"{el / frames * 1e3:.1f} ms/frame, oracle/pt_oracle.c single thread",
-            "ms_per_frame": round(el / frames * 1e3, 2)}
+
+    def run(threads, seconds):
+        r = O.Renderer(sc, O.options(num_threads=threads))
+        segs, frames, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds or frames < 2:
+            frames += 1
+            segs += int(np.maximum(r.trace(frames), 0).sum())
+        el = time.perf_counter() - t0
+        return segs / el / 1e6, frames, el
+
+    v1, f1, e1 = run(1, budget_s)
+    nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    vn, fn, en = run(nt, budget_s / 2)
+    return {"value": round(v1, 3), "unit": "Mpaths/s", "cores": 1, "kind": "port",
+            "sample": f"cornell.json 400x400 depth 4 (BASELINE configs[0]), {f1} frames in {e1:.1f} s, "
+                      f"{e1 / f1 * 1e3:.1f} ms/frame, oracle/pt_oracle.c single thread",
+            "ms_per_frame": round(e1 / f1 * 1e3, 2),
+            "multithread": {"value": round(vn, 3), "unit": "Mpaths/s", "cores": nt,
+                            "sample": f"same workload, {fn} frames in {en:.1f} s, OpenMP over paths"}}
 
 
 if __name__ == "__main__":
