@@ -427,21 +427,29 @@ PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_node
         // triangle, which intersectTriangle rejects (det = 0) or reports with t = NaN (NaN
         // ray), and `t > 0` never accepts
         // (positions only: the third record word is read as one float, v2.z)
+        // two slots at a time (the second pair's loads issue while the first pair is tested):
+        // half the triangle registers live, one more wave per SIMD
         const int base = 4 * (cur - P);
-        float4 ta[4], tb[4];
-        float tc[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            ta[i] = sc.hot4[base + i].a;
-            tb[i] = sc.hot4[base + i].b;
-            tc[i] = sc.hot4[base + i].c.x;
-        }
         if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
+        float4 ta[2], tb[2];
+        float tc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            ta[j] = sc.hot4[base + j].a;
+            tb[j] = sc.hot4[base + j].b;
+            tc[j] = sc.hot4[base + j].c.x;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const f3 v0 = mk(ta[i].x, ta[i].y, ta[i].z);
-            const f3 v1 = mk(ta[i].w, tb[i].x, tb[i].y);
-            const f3 v2 = mk(tb[i].z, tb[i].w, tc[i]);
+            const int j = i & 1;
+            const f3 v0 = mk(ta[j].x, ta[j].y, ta[j].z);
+            const f3 v1 = mk(ta[j].w, tb[j].x, tb[j].y);
+            const f3 v2 = mk(tb[j].z, tb[j].w, tc[j]);
+            if (i < 2) {                       // refill this slot with triangle i + 2
+                ta[j] = sc.hot4[base + i + 2].a;
+                tb[j] = sc.hot4[base + i + 2].b;
+                tc[j] = sc.hot4[base + i + 2].c.x;
+            }
             float t, u, v;
             if (tri_test(st.ro, st.rd, v0, v1, v2, t, u, v) && t > 0.0f &&
                 (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
