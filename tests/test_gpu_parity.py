@@ -308,6 +308,21 @@ def test_full_resolution_mesh_fast_bvh(name, oracle, ptamd):
     tr.free()
 
 
+def test_prepared_graphs_equal_oracle(oracle, ptamd):
+    """pt_prepare_frames captures the pass graphs a later pt_trace_frames replays (bench.py keeps
+    the capture out of its timed region); the frames traced through them equal the oracle."""
+    a, b = _oracle_pair(oracle, ptamd, "cornell_glass_test", (40, 40))
+    tr = ptamd.PathTracer(b, frames_per_pass=4)
+    tr.prepare_frames(7)                       # passes of 4 and 3
+    tr.trace_frames(1, 7)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in range(1, 8):
+        r.trace(it)
+    assert tr.stats()["frames_total"] == 7
+    assert _eq(tr.image(), r.image)
+    tr.free()
+
+
 def test_graph_replay_equals_eager(oracle, ptamd):
     a, b = _oracle_pair(oracle, ptamd, "cornell_glass_test", (96, 96))
     imgs = []
