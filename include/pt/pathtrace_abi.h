@@ -82,8 +82,10 @@ typedef struct pt_options {
                                     tests, near-first order and certified t-culling, 32: rays
                                     that enter the mesh's root box are queued and traversed in
                                     full waves by a second kernel per bounce, 64: keep 16 on the
-                                    reference node array instead of the paired-children layout);
-                                    results are bit-identical for every value.  Default 2|8|16|32 */
+                                    reference node array instead of the paired-children layout,
+                                    128: with 8, the exact-test exchange spans the whole block);
+                                    results are bit-identical for every value.  Default
+                                    2|8|16|32|128 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..32;
                                     0 = auto: ~21M paths in flight).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in

@@ -31,6 +31,7 @@ enum : int {
     VAR_BVH_SPLIT = 32,    // fused + BVH_FAST + pair layout: rays that enter the mesh's root box are
                            // queued and traversed (then shaded) by k_bvh_bounce in full waves
     VAR_BVH_NODES = 64,    // host only: BVH_FAST on the node array instead of the DevPair layout (A/B)
+    VAR_BLOCK_REDIST = 128,  // with VAR_WAVE_REDIST: the exchange spans the block (block_intersect)
 };
 
 struct CamDev {
@@ -803,6 +804,7 @@ struct WaveLds {
     float rt[WCAP], rs[3][WCAP];
     uint16_t task[WCAP];
 };
+template <bool COUNT = false>
 PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, WaveLds* W,
                            float& t_min, int& win, f3& seed) {
     const int lane = threadIdx.x & 63;
@@ -834,6 +836,14 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
     t_min = FLT_MAX_;
     win = -1;
     seed = mk(0.f, 0.f, 0.f);
+    if (COUNT) {   // tools/section_times.py: exchanged pairs and rounds per wave, sphere pairs
+        sec_add(SEC_N_ITERS, (uint64_t)((total + 63) / 64));
+        sec_add(SEC_N_EXACT, (uint64_t)total);
+        sec_add(SEC_N_BVH_RAYS, 1);                 // waves through the exchange
+        int sph = 0;
+        for (uint64_t m = cand; m; m &= m - 1) sph += sc.geoms[__builtin_ctzll(m)].type != PT_CUBE;
+        sec_add_lanes(SEC_N_CAND, sph);
+    }
     if (total > WCAP) {                          // rare: per-lane queue (same results)
         while (__any(cand != 0)) {
             if (cand != 0) {
@@ -886,6 +896,108 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
             t_min = t;
             win = W->task[j] & 255;
             seed = mk(W->rs[0][j], W->rs[1][j], W->rs[2][j]);
+        }
+    }
+}
+
+// VAR_BLOCK_REDIST: wave_intersect's exchange across the whole block.  The four waves' (ray,
+// geom) pairs form one list in (lane, geom) order; wave w takes entries w*64 + r*256 + lane, so
+// the block runs ceil(pairs / 64) wave-rounds of exact tests instead of the sum over its waves
+// of ceil(wave pairs / 64) (cornell: 79 pairs per wave on average -> 1.67 rounds each).  Same
+// per-lane scan of its own results afterwards, so the winner is unchanged.  Every thread of the
+// block must call it.
+constexpr int BCAP = 4 * WCAP;
+struct BlockLds {
+    float ro[3][BLOCK], rd[3][BLOCK];
+    float rt[BCAP], rs[3][BCAP];
+    uint16_t task[BCAP];
+    int wsum[BLOCK / 64];
+};
+PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, BlockLds* B,
+                            float& t_min, int& win, f3& seed) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint64_t cand = 0;
+    CullRay cr;
+    if (live) {
+        cr = cull_ray(ro, rd);
+        const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
+                             __builtin_fabsf(rd.z) <= 1e3f;
+#pragma unroll 4
+        for (int i = 0; i < sc.num_geoms; ++i)
+            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) {
+                const int a = sc.geoms[i].away_axis;
+                if (!(a >= 0 && bounded && away_on_axis(sc.geoms[i], a, ro, rd))) cand |= 1ull << i;
+            }
+    }
+    const int cnt = __builtin_popcountll(cand);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) B->wsum[w] = incl;
+    __syncthreads();
+    int woff = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; ++i) {
+        const int x = B->wsum[i];
+        woff += i < w ? x : 0;
+        total += x;
+    }
+    const int excl = woff + incl - cnt;
+    t_min = FLT_MAX_;
+    win = -1;
+    seed = mk(0.f, 0.f, 0.f);
+    if (total > BCAP) {                          // block-uniform, rare: per-lane queue (same results)
+        while (__any(cand != 0)) {
+            if (cand != 0) {
+                const int i = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const DevGeom& g = lg[i];
+                if (!cull_geom(g, cr, t_min)) {
+                    f3 s;
+                    const float t = geom_test(g, ro, rd, s);
+                    if (t > 0.0f && t_min > t) {
+                        t_min = t;
+                        win = i;
+                        seed = s;
+                    }
+                }
+            }
+        }
+        return;
+    }
+    B->ro[0][tid] = ro.x;
+    B->ro[1][tid] = ro.y;
+    B->ro[2][tid] = ro.z;
+    B->rd[0][tid] = rd.x;
+    B->rd[1][tid] = rd.y;
+    B->rd[2][tid] = rd.z;
+    {
+        int j = excl;
+        for (uint64_t m = cand; m; m &= m - 1) B->task[j++] = (uint16_t)((tid << 8) | __builtin_ctzll(m));
+    }
+    __syncthreads();
+    for (int k = w * 64 + lane; k < total; k += BLOCK) {
+        const int task = B->task[k];
+        const int src = task >> 8, gi = task & 255;
+        const f3 o = mk(B->ro[0][src], B->ro[1][src], B->ro[2][src]);
+        const f3 d = mk(B->rd[0][src], B->rd[1][src], B->rd[2][src]);
+        f3 s;
+        const float t = geom_test(lg[gi], o, d, s);
+        B->rt[k] = t;
+        B->rs[0][k] = s.x;
+        B->rs[1][k] = s.y;
+        B->rs[2][k] = s.z;
+    }
+    __syncthreads();
+    for (int j = excl; j < excl + cnt; ++j) {
+        const float t = B->rt[j];
+        if (t > 0.0f && t_min > t) {
+            t_min = t;
+            win = B->task[j] & 255;
+            seed = mk(B->rs[0][j], B->rs[1][j], B->rs[2][j]);
         }
     }
 }

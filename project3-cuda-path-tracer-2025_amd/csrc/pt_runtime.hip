@@ -237,7 +237,11 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     int qw = -1;
     f3 qs = mk(0.f, 0.f, 0.f);
     if (REDIST && lds_geoms) {                     // wave-cooperative: every lane takes part
-        wave_intersect(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
+        if (VAR & VAR_BLOCK_REDIST)
+            block_intersect(sc, s_geoms, live, p.o, p.d, reinterpret_cast<BlockLds*>(s_wave_isect - (tid >> 6)), qt,
+                            qw, qs);
+        else
+            wave_intersect<TIMING>(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
     } else if (SPLIT && live) {
         prim_intersect_q<TIMING, FIRST && !TIMING>(sc, s_geoms, p.o, p.d, qt, qw, qs);
     }
@@ -819,7 +823,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
     const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && g.sc.num_geoms <= LDS_GEOMS;
     const size_t geom_lds = lds ? sizeof(DevGeom) * g.sc.num_geoms : 0;
-    const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds ? sizeof(WaveLds) * (BLOCK / 64) : 0;
+    const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds
+                                  ? std::max(sizeof(WaveLds) * (BLOCK / 64), (VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : 0)
+                                  : 0;
     const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
     launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + redist_lds, g.sc, in, out,
            g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
@@ -841,13 +847,16 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 50: launch_bounce_t<FIRST, HAS_BVH, 50>(grid, in, out, b); break;
         case 58: launch_bounce_t<FIRST, HAS_BVH, 58>(grid, in, out, b); break;
         case 54: launch_bounce_t<FIRST, HAS_BVH, 54>(grid, in, out, b); break;   // split + section counters
+        case 30: launch_bounce_t<FIRST, HAS_BVH, 30>(grid, in, out, b); break;   // redist + pair counters
+        case 154: launch_bounce_t<FIRST, HAS_BVH, 154>(grid, in, out, b); break;
+        case 186: launch_bounce_t<FIRST, HAS_BVH, 186>(grid, in, out, b); break;
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
 void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
     // camera rays of neighbouring pixels share their candidates: redistribution only costs there
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
-    if (first) var &= ~VAR_WAVE_REDIST;
+    if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
     if (!g.split) var &= ~VAR_BVH_SPLIT;
     if (first) {
         if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
@@ -880,7 +889,7 @@ int enqueue_pass_body(int batch) {
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
         for (int b = 0; b < nbounces; ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & 63, dim3(nb), in, out, b);
+            launch_bounce(b == 0, g.has_bvh, g.opts.variant & ~VAR_BVH_NODES, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -1099,7 +1108,7 @@ void pt_default_options(pt_options* o) {
     o->shard_rows = 8;
     o->block_size = BLOCK;
     // fastest in the in-process A/B (tools/ab_variants.py); every variant is bit-identical
-    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BVH_SPLIT;
+    o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BVH_SPLIT | VAR_BLOCK_REDIST;
     o->frames_per_pass = 0;        // auto
 }
 

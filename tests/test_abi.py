@@ -30,7 +30,7 @@ def test_version_and_defaults(ptamd):
     o = ptamd.default_options()
     # the reference's compile-time defaults, pathtrace.cu:20-24
     assert (o.stream_compaction, o.material_sort, o.bvh) == (1, 0, 1)
-    assert o.block_size == 256 and o.use_graph == 1 and o.pipeline == 0 and o.variant == 58
+    assert o.block_size == 256 and o.use_graph == 1 and o.pipeline == 0 and o.variant == 186
 
 
 def test_call_order_errors(ptamd):

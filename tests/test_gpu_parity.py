@@ -193,6 +193,10 @@ FRAME_CASES = [
     ("cornell_obj_khaslana", (48, 48), 12, {"variant": 26}),
     ("cornell_obj_bnnuy", (64, 64), None, {"variant": 90}),             # fast BVH on the node array
     ("cornell_obj_khaslana", (48, 48), 12, {"variant": 90, "pipeline": 1}),
+    ("cornell", (64, 64), None, {"variant": 154}),                      # block-wide exchange
+    ("cornell_glass_test", (64, 64), None, {"variant": 154}),
+    ("cornell_obj_khaslana", (48, 48), 12, {"variant": 58}),             # per-wave exchange
+    ("synthetic_textured_bump", (48, 48), None, {"variant": 58}),
     ("cornell_obj_bnnuy", (64, 64), None, {"variant": 58}),             # split: traversal queue kernel
     ("cornell_obj_khaslana", (48, 48), 12, {"variant": 58}),
     ("synthetic_textured_bump", (48, 48), None, {"variant": 58}),
