@@ -124,6 +124,7 @@ struct DevGeom {
 };
 static_assert(sizeof(DevGeom) == 192, "DevGeom");
 
+
 // geom_test's cube early-out, on ONE object axis a, with geom_test's own arithmetic for qo[a]
 // and u[a] (xform row a).  True only when geom_test would return -1 through that early-out: the
 // object-space origin is outside slab a and the direction points away.  u[a]'s w term

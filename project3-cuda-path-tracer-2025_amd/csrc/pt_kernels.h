@@ -798,6 +798,17 @@ PT_DEV void tex_fetch(const SceneDev& sc, int id, float x, float y, float out[4]
 // instead of max-over-lanes(candidates).  Each lane then scans its own pairs in geom order with
 // the reference's `t > 0 && t_min > t` rule, so the winner (first minimum) is unchanged.  Every
 // lane of the wave must call this (uniform control flow); `live` = the lane has a ray.
+// candidates the exchanged exact test would certainly reject: a cube the ray leaves through
+// geom_test's own "away" early-out (away_on_axis).  `bounded`: |rd| components <= 1e3
+// (away_on_axis' precondition).  Spheres keep theirs: most sphere candidates are rays leaving
+// the sphere, whose exact test can round to a self-hit at t ~ 1e-4 (t1 = -b + sqrt(b^2 - ~0) =
+// 0), so only the reference arithmetic can reject them (a bounding-ball line test dropped 3 % of
+// all pairs and bought nothing).
+PT_DEV bool certain_exact_miss(const DevGeom& g, f3 ro, f3 rd, bool bounded) {
+    const int a = g.away_axis;
+    return g.type == PT_CUBE && (unsigned)a < 3u && bounded && away_on_axis(g, a, ro, rd);
+}
+
 constexpr int WCAP = 192;      // pairs per wave held in LDS; more -> per-lane queue fallback
 struct WaveLds {
     float ro[3][64], rd[3][64];
@@ -819,10 +830,8 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
                              __builtin_fabsf(rd.z) <= 1e3f;
 #pragma unroll 4
         for (int i = 0; i < sc.num_geoms; ++i)
-            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) {
-                const int a = sc.geoms[i].away_axis;
-                if (!(a >= 0 && bounded && away_on_axis(sc.geoms[i], a, ro, rd))) cand |= 1ull << i;
-            }
+            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_) && !certain_exact_miss(sc.geoms[i], ro, rd, bounded))
+                cand |= 1ull << i;
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;
@@ -924,10 +933,8 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
                              __builtin_fabsf(rd.z) <= 1e3f;
 #pragma unroll 4
         for (int i = 0; i < sc.num_geoms; ++i)
-            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_)) {
-                const int a = sc.geoms[i].away_axis;
-                if (!(a >= 0 && bounded && away_on_axis(sc.geoms[i], a, ro, rd))) cand |= 1ull << i;
-            }
+            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_) && !certain_exact_miss(sc.geoms[i], ro, rd, bounded))
+                cand |= 1ull << i;
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;
