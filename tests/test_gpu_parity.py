@@ -312,6 +312,41 @@ def test_full_resolution_mesh_fast_bvh(name, oracle, ptamd):
     tr.free()
 
 
+def _many_geoms_scene(path, n):
+    """cornell.json plus n small cubes / spheres (mixed materials, some rotated and scaled
+    non-uniformly): more geoms than the fused kernel stages in LDS (LDS_GEOMS = 64), so the
+    global-table intersection path runs."""
+    with open(scene_path("cornell")) as f:
+        d = json.load(f)
+    d["Materials"]["mirror"] = {"RGB": [0.9, 0.9, 0.9], "TYPE": "Specular"}
+    d["Materials"]["glass"] = {"RGB": [0.95, 0.95, 0.95], "TYPE": "Refractive", "IOR": 1.5}
+    rng = np.random.default_rng(7)
+    mats = ["diffuse_red", "diffuse_green", "diffuse_white", "mirror", "glass"]
+    for i in range(n):
+        d["Objects"].append({"TYPE": "cube" if i % 2 else "sphere", "MATERIAL": mats[i % len(mats)],
+                             "TRANS": [float(x) for x in rng.uniform([-4, 0.5, -4], [4, 9, 3])],
+                             "ROTAT": [float(x) for x in rng.uniform(0, 90, 3)],
+                             "SCALE": [float(x) for x in rng.uniform(0.2, 0.9, 3)]})
+    with open(path, "w") as f:
+        json.dump(d, f)
+    return str(path)
+
+
+@pytest.mark.parametrize("opts", [{}, {"pipeline": 1}, {"variant": 10}])
+def test_more_geoms_than_lds_table(opts, tmp_path, oracle, ptamd):
+    path = _many_geoms_scene(tmp_path / "many.json", 72)
+    a, b = _oracle_pair(oracle, ptamd, path, (48, 48))
+    assert len(b.geoms) > 64
+    tr = ptamd.PathTracer(b, **opts)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in (1, 2):
+        r.trace(it)
+        tr.trace(it)
+    assert _eq(tr.image(), r.image)
+    assert np.isfinite(r.image).mean() > 0.99 and r.image.sum() > 0
+    tr.free()
+
+
 def test_prepared_graphs_equal_oracle(oracle, ptamd):
     """pt_prepare_frames captures the pass graphs a later pt_trace_frames replays (bench.py keeps
     the capture out of its timed region); the frames traced through them equal the oracle."""
