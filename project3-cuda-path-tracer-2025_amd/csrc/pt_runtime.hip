@@ -586,29 +586,40 @@ __global__ __launch_bounds__(BLOCK) void k_sort_hist(const int* __restrict__ key
     for (int i = threadIdx.x; i < nkeys; i += BLOCK) tile_hist[(size_t)tile * nkeys + i] = h[i];
 }
 
-// exclusive scan over (key, tile) in key-major order; one block
-__global__ __launch_bounds__(BLOCK) void k_sort_scan(int* tile_hist, const int* n_ptr, int nkeys) {
+// exclusive scan over (key, tile) in key-major order: one block of SCAN_THREADS, each thread a
+// contiguous run of the flattened (key, tile) index space (tile_hist is stored [tile][key]),
+// then a block scan of the run sums.  (The earlier one-thread-per-key loop over all tiles ran
+// ~780 us at 10k tiles: 5-27 busy threads out of 256.)
+__global__ __launch_bounds__(SCAN_THREADS) void k_sort_scan(int* tile_hist, const int* n_ptr, int nkeys) {
+    __shared__ int s_part[SCAN_THREADS];
     const int n = *n_ptr;
     const int ntiles = (n + STILE - 1) / STILE;
-    __shared__ int key_tot[MAXMAT];
-    __shared__ int key_off[MAXMAT];
-    for (int key = threadIdx.x; key < nkeys; key += BLOCK) {
-        int s = 0;
-        for (int t = 0; t < ntiles; ++t) {
-            int c = tile_hist[(size_t)t * nkeys + key];
-            tile_hist[(size_t)t * nkeys + key] = s;
-            s += c;
-        }
-        key_tot[key] = s;
+    const int total = ntiles * nkeys;
+    const int per = (total + SCAN_THREADS - 1) / SCAN_THREADS;
+    const int tid = threadIdx.x;
+    const int lo = min(total, tid * per), hi = min(total, lo + per);
+    const int key0 = ntiles ? lo / ntiles : 0, t0 = lo - key0 * ntiles;
+    int sum = 0;
+    for (int f = lo, key = key0, t = t0; f < hi; ++f) {
+        sum += tile_hist[(size_t)t * nkeys + key];
+        if (++t == ntiles) { t = 0; ++key; }
     }
+    s_part[tid] = sum;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int k = 0; k < nkeys; ++k) { key_off[k] = run; run += key_tot[k]; }
+    for (int off = 1; off < SCAN_THREADS; off <<= 1) {   // Hillis-Steele inclusive scan in LDS
+        const int v = tid >= off ? s_part[tid - off] : 0;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
     }
-    __syncthreads();
-    for (int key = threadIdx.x; key < nkeys; key += BLOCK)
-        for (int t = 0; t < ntiles; ++t) tile_hist[(size_t)t * nkeys + key] += key_off[key];
+    int run = tid ? s_part[tid - 1] : 0;
+    for (int f = lo, key = key0, t = t0; f < hi; ++f) {
+        const size_t at = (size_t)t * nkeys + key;
+        const int c = tile_hist[at];
+        tile_hist[at] = run;
+        run += c;
+        if (++t == ntiles) { t = 0; ++key; }
+    }
 }
 
 // stable scatter: rank among equal keys = earlier items of the tile (item order k-major, wave,
@@ -915,7 +926,7 @@ int enqueue_pass_body(int batch) {
         if (g.opts.material_sort) {
             const int nk = std::max(1, g.sc.num_mats);
             launch(4, k_sort_hist, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.d_tile_hist);
-            launch(4, k_sort_scan, dim3(1), dim3(BLOCK), 0, g.d_tile_hist, n_in, nk);
+            launch(4, k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, g.d_tile_hist, n_in, nk);
             launch(4, k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.key_bits,
                    (const int*)g.d_tile_hist, g.d_perm);
             HIPCHK(hipGetLastError());
@@ -1875,7 +1886,7 @@ int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm)
     const int ntiles = (int)((n + STILE - 1) / STILE);
     hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
                        g.d_tile_hist);
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(BLOCK), 0, g.stream, g.d_tile_hist, staged_count(0), nk);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, g.stream, g.d_tile_hist, staged_count(0), nk);
     hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
                        g.key_bits, g.d_tile_hist, g.d_perm);
     HIPCHK(hipGetLastError());
