@@ -19,6 +19,8 @@
 #include "pt/pt_libm.h"
 #include "pt/scene_structs.h"
 
+typedef float v4f __attribute__((ext_vector_type(4)));   // native vector: one dwordx4 load
+
 #define PT_DEV __device__ __forceinline__
 
 namespace ptd {
@@ -290,10 +292,9 @@ PT_DEV float geom_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
     return length(ro - p);
 }
 
-// Moller-Trumbore, intersections.cu:112-145
-PT_DEV bool tri_test(f3 ro, f3 rd, f3 v0, f3 v1, f3 v2, float& tOut, float& uOut, float& vOut) {
-    f3 edge1 = v1 - v0;
-    f3 edge2 = v2 - v0;
+// Moller-Trumbore, intersections.cu:112-145, from v0 and the two edges v1 - v0, v2 - v0 (float
+// differences: the leaf records hold them precomputed with the same single rounding)
+PT_DEV bool tri_test_e(f3 ro, f3 rd, f3 v0, f3 edge1, f3 edge2, float& tOut, float& uOut, float& vOut) {
     f3 pvec = cross(rd, edge2);
     float det = dot(edge1, pvec);
     if (__builtin_fabsf(det) < BABY_EPSILON) return false;
@@ -308,6 +309,9 @@ PT_DEV bool tri_test(f3 ro, f3 rd, f3 v0, f3 v1, f3 v2, float& tOut, float& uOut
     if (t <= BABY_EPSILON) return false;
     tOut = t; uOut = u; vOut = v;
     return true;
+}
+PT_DEV bool tri_test(f3 ro, f3 rd, f3 v0, f3 v1, f3 v2, float& tOut, float& uOut, float& vOut) {
+    return tri_test_e(ro, rd, v0, v1 - v0, v2 - v0, tOut, uOut, vOut);
 }
 
 // aabbIntersectionTest, intersections.cu:237-275

@@ -65,6 +65,7 @@ struct SceneDev {
     // VAR_BVH_FAST layout (pairs != null when the tree allows it, see DevPair)
     const DevPair* pairs;
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
+    const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
@@ -424,35 +425,22 @@ PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_node
             next = true;
         }
     } else {
-        // all four slots, loads issued together: unused slots hold a degenerate (all-zero)
-        // triangle, which intersectTriangle rejects (det = 0) or reports with t = NaN (NaN
-        // ray), and `t > 0` never accepts
-        // (positions only: the third record word is read as one float, v2.z)
-        // two slots at a time (the second pair's loads issue while the first pair is tested):
-        // half the triangle registers live, one more wave per SIMD
-        const int base = 4 * (cur - P);
+        // the leaf's 4 slots as 9 float4 (component k of slots 0..3): 9 dwordx4 loads, and the
+        // edges v1 - v0, v2 - v0 come precomputed (same float rounding).  Unused slots are
+        // all-zero (det = 0: rejected; a NaN ray gets t = NaN, which `t > 0` never accepts).
+        const int leaf = cur - P, base = 4 * leaf;
         if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
-        float4 ta[2], tb[2];
-        float tc[2];
+        const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
+        v4f c[9];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            ta[j] = sc.hot4[base + j].a;
-            tb[j] = sc.hot4[base + j].b;
-            tc[j] = sc.hot4[base + j].c.x;
-        }
+        for (int k = 0; k < 9; ++k) c[k] = L[k];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int j = i & 1;
-            const f3 v0 = mk(ta[j].x, ta[j].y, ta[j].z);
-            const f3 v1 = mk(ta[j].w, tb[j].x, tb[j].y);
-            const f3 v2 = mk(tb[j].z, tb[j].w, tc[j]);
-            if (i < 2) {                       // refill this slot with triangle i + 2
-                ta[j] = sc.hot4[base + i + 2].a;
-                tb[j] = sc.hot4[base + i + 2].b;
-                tc[j] = sc.hot4[base + i + 2].c.x;
-            }
+            const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
+            const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
+            const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
             float t, u, v;
-            if (tri_test(st.ro, st.rd, v0, v1, v2, t, u, v) && t > 0.0f &&
+            if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
                 (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
                 st.t_hit = t;
                 st.bu = u;

@@ -500,7 +500,6 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_compact_scan(const int* __rest
 
 // native 4-float vector: arrays of it stay in VGPRs (HIP's float4 is a union wrapper, and
 // arrays of it were demoted to LDS/scratch, serialising each item's loads behind a wait)
-typedef float v4f __attribute__((ext_vector_type(4)));
 
 template <int CITEMS>
 __global__ __launch_bounds__(BLOCK) void k_compact_scatter(const float4* __restrict__ inA, const float4* __restrict__ inB,
@@ -752,6 +751,7 @@ struct State {
     DevTriHot* d_hot = nullptr;
     DevPair* d_pairs = nullptr;
     DevTriHot* d_hot4 = nullptr;
+    float4* d_leaf9 = nullptr;
     DevTriCold* d_cold = nullptr;
     float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     float4* d_hit_nt = nullptr;
@@ -1009,7 +1009,7 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
+    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
                     g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl,
                     g.queue.A, g.queue.B, g.queue.C, g.queue.D};
     for (void* p : ptrs)
@@ -1297,6 +1297,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     std::vector<DevTriCold> cold;
     std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
     std::vector<DevTriHot> hot4;
+    std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0;
     float4 pair_root_lo{}, pair_root_hi{};
     double cull_extent = 1.0;
@@ -1497,6 +1498,22 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                     const int cnt = nd.triCount;
                     memcpy(&hot4[4 * (size_t)k].c.z, &cnt, 4);
                 }
+                // trav_step's leaf records: component k of the 4 slots in one float4, positions
+                // as v0 and the float edges v1 - v0, v2 - v0 (tri_test's own first rounding)
+                leaf9.assign(9 * (size_t)L, make_float4(0.f, 0.f, 0.f, 0.f));
+                for (int k = 0; k < L; ++k)
+                    for (int i = 0; i < 4; ++i) {
+                        const DevTriHot& h = hot4[4 * (size_t)k + i];
+                        const float v0[3] = {h.a.x, h.a.y, h.a.z}, v1[3] = {h.a.w, h.b.x, h.b.y},
+                                    v2[3] = {h.b.z, h.b.w, h.c.x};
+                        float comp9[9];
+                        for (int a = 0; a < 3; ++a) {
+                            comp9[a] = v0[a];
+                            comp9[3 + a] = v1[a] - v0[a];
+                            comp9[6 + a] = v2[a] - v0[a];
+                        }
+                        for (int m = 0; m < 9; ++m) (&leaf9[9 * (size_t)k + m].x)[i] = comp9[m];
+                    }
                 pair_root_ref = ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
@@ -1538,6 +1555,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             RC(upload(g.d_pairs, pairs.data(), pairs.size()));
             RC(dalloc(&g.d_hot4, hot4.size()));
             RC(upload(g.d_hot4, hot4.data(), hot4.size()));
+            RC(dalloc(&g.d_leaf9, leaf9.size()));
+            RC(upload(g.d_leaf9, leaf9.data(), leaf9.size()));
         }
     }
     for (int i = 0; i < 2; ++i)
@@ -1612,6 +1631,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.num_textures = num_tex;
     sc.pairs = g.d_pairs;
     sc.hot4 = g.d_hot4;
+    sc.leaf9 = g.d_leaf9;
     sc.num_pairs = pair_count;
     sc.root_ref = pair_root_ref;
     sc.root_lo = pair_root_lo;
