@@ -311,11 +311,13 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
 // (bvh_intersect_pairs via finish_hit, entering with their primitive winner), are shaded, and
 // gathered / compacted into the same output segments as k_bounce (blockIdx % NSEG; the host
 // doubles seg_stride so both kernels' survivors fit).
-// __launch_bounds__(256, 5): 5 waves per SIMD (<= 96 VGPRs, a few bytes of scratch in cold
-// paths) beat 4 waves at 104 VGPRs by ~10 % on this latency-bound traversal; 6 waves (80 VGPRs)
-// spill more and lose it again (bunny 0.607 -> 0.561 -> 0.564 ms/frame)
+// __launch_bounds__(256, 7): 7 waves per SIMD (<= 72 VGPRs; a few bytes of scratch in the cold
+// exact-fallback paths).  Occupancy is what this latency-bound traversal lives on: with the SLP
+// vectorizer on (packed-f32 pairs built from duplicated registers) it needed 96 VGPRs for 5
+// waves; without it (Makefile) 79 VGPRs natural, and 72 at this bound (bunny 0.489 -> 0.477
+// ms/frame); 8 waves (64 VGPRs) spill 100 B
 template <int VAR>
-__global__ __launch_bounds__(BLOCK, 5) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK, 7) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
                                                       float* __restrict__ image, int bounce, int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
     const int n = ctl->qcnt[bounce][0];
