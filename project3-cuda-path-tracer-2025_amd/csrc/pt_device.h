@@ -127,6 +127,18 @@ struct DevGeom {
 static_assert(sizeof(DevGeom) == 192, "DevGeom");
 
 
+// Per-geom record of the candidate pre-test (block_intersect / wave_intersect), 48 bytes read
+// as 3 float4 with no branch between them: the conservative world box of cull_geom, and the
+// inverse-matrix row of away_on_axis's axis (all zero, never "away", for spheres and for cubes
+// without one).
+struct DevCull {
+    float lo[3], hi[3];
+    float row[4];          // inv[a], inv[3 + a], inv[6 + a], inv[9 + a]
+    int32_t has_row;       // 1: a cube with an away axis (row valid)
+    float _pad;
+};
+static_assert(sizeof(DevCull) == 48, "DevCull");
+
 // geom_test's cube early-out, on ONE object axis a, with geom_test's own arithmetic for qo[a]
 // and u[a] (xform row a).  True only when geom_test would return -1 through that early-out: the
 // object-space origin is outside slab a and the direction points away.  u[a]'s w term

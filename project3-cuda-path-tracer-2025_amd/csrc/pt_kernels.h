@@ -49,6 +49,7 @@ struct ShardDev {
 
 struct SceneDev {
     const DevGeom* geoms;
+    const DevCull* cull;      // candidate pre-test records, one per geom
     const DevMaterial* mats;
     const DevNode* nodes;
     const DevTriHot* hot;
@@ -796,6 +797,28 @@ PT_DEV bool certain_exact_miss(const DevGeom& g, f3 ro, f3 rd, bool bounded) {
     const int a = g.away_axis;
     return g.type == PT_CUBE && (unsigned)a < 3u && bounded && away_on_axis(g, a, ro, rd);
 }
+// !cull_geom<false>(g) && !certain_exact_miss(g) from geom i's DevCull record, its three loads
+// issued together ahead of any branch: same slab arithmetic as cull_geom, same qo / u arithmetic
+// as away_on_axis (only for records with an away row, on the lanes the box test kept)
+PT_DEV bool cull_keep(const SceneDev& sc, int i, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
+    const float4* rec = reinterpret_cast<const float4*>(sc.cull) + 3 * i;
+    const float4 A = rec[0], B = rec[1], C = rec[2];   // lo.xyz hi.x | hi.yz row0 row1 | row2 row3 - -
+    const float a0 = __builtin_fmaf(A.x, cr.id.x, -cr.rid.x), b0 = __builtin_fmaf(A.w, cr.id.x, -cr.rid.x);
+    const float a1 = __builtin_fmaf(A.y, cr.id.y, -cr.rid.y), b1 = __builtin_fmaf(B.x, cr.id.y, -cr.rid.y);
+    const float a2 = __builtin_fmaf(A.z, cr.id.z, -cr.rid.z), b2 = __builtin_fmaf(B.y, cr.id.z, -cr.rid.z);
+    const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                     __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
+    const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                     __builtin_fmaxf(a2, b2));
+    bool keep = t1 >= t0;
+    if (__float_as_int(C.z) != 0 && keep) {   // a record with an away row, lanes still keeping it
+        const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
+        const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
+        const bool away = (qo > 0.5f && u > 0.0f) || (qo < -0.5f && u < 0.0f);
+        keep = keep && !(bounded && away);
+    }
+    return keep;
+}
 
 constexpr int WCAP = 192;      // pairs per wave held in LDS; more -> per-lane queue fallback
 struct WaveLds {
@@ -818,8 +841,7 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
                              __builtin_fabsf(rd.z) <= 1e3f;
 #pragma unroll 4
         for (int i = 0; i < sc.num_geoms; ++i)
-            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_) && !certain_exact_miss(sc.geoms[i], ro, rd, bounded))
-                cand |= 1ull << i;
+            if (cull_keep(sc, i, cr, ro, rd, bounded)) cand |= 1ull << i;
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;
@@ -921,8 +943,7 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
                              __builtin_fabsf(rd.z) <= 1e3f;
 #pragma unroll 4
         for (int i = 0; i < sc.num_geoms; ++i)
-            if (!cull_geom<false>(sc.geoms[i], cr, FLT_MAX_) && !certain_exact_miss(sc.geoms[i], ro, rd, bounded))
-                cand |= 1ull << i;
+            if (cull_keep(sc, i, cr, ro, rd, bounded)) cand |= 1ull << i;
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;

@@ -747,6 +747,7 @@ struct State {
     size_t bvh_lds = 0;
     // device buffers
     DevGeom* d_geoms = nullptr;
+    DevCull* d_cull = nullptr;
     DevMaterial* d_mats = nullptr;
     float4* d_node_aux = nullptr;
     DevNode* d_nodes = nullptr;
@@ -1011,7 +1012,7 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
+    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
                     g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl,
                     g.queue.A, g.queue.B, g.queue.C, g.queue.D};
     for (void* p : ptrs)
@@ -1269,6 +1270,21 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                 d.box_lo[r] = std::nextafter(bc[3 * i + r] - h, -INFINITY);
                 d.box_hi[r] = std::nextafter(bc[3 * i + r] + h, INFINITY);
             }
+        }
+    }
+    std::vector<DevCull> culls(std::max(1, s->num_geoms));
+    for (int i = 0; i < s->num_geoms; ++i) {
+        const DevGeom& d = geoms[i];
+        DevCull& c = culls[i];
+        memset(&c, 0, sizeof c);
+        for (int r = 0; r < 3; ++r) {
+            c.lo[r] = d.box_lo[r];
+            c.hi[r] = d.box_hi[r];
+        }
+        const int a = d.away_axis;
+        if (d.type == PT_CUBE && a >= 0 && a < 3) {
+            for (int k = 0; k < 4; ++k) c.row[k] = d.inv[3 * k + a];
+            c.has_row = 1;
         }
     }
     std::vector<DevMaterial> mats(std::max(1, s->num_materials));
@@ -1542,6 +1558,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     RC(dalloc(&g.d_geoms, geoms.size()));
     RC(dalloc(&g.d_mats, mats.size()));
     RC(upload(g.d_geoms, geoms.data(), geoms.size()));
+    RC(dalloc(&g.d_cull, culls.size()));
+    RC(upload(g.d_cull, culls.data(), culls.size()));
     RC(upload(g.d_mats, mats.data(), mats.size()));
     if (g.has_bvh) {
         RC(dalloc(&g.d_nodes, nodes.size()));
@@ -1612,6 +1630,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
 
     SceneDev& sc = g.sc;
     sc.geoms = g.d_geoms;
+    sc.cull = g.d_cull;
     sc.mats = g.d_mats;
     sc.nodes = g.d_nodes;
     sc.node_aux = g.d_node_aux;
