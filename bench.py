@@ -130,6 +130,7 @@ def main():
         tr.reset_stats()
         prof = tr.profile(it + args.steps, args.steps)
         st_prof = tr.stats()
+        spread = pass_spread(tr, it + 2 * args.steps, st_prof["frames_per_pass"])
     if world > 1:
         t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         tmax = t.clone()
@@ -178,6 +179,8 @@ def main():
                                "per_launch_bounce_ms": [round(x, 4) for x in prof["bounce_ms"]],
                                "per_launch_bvh_ms": [round(x, 4) for x in prof["bvh_ms"]],
                                "combine_ms_per_frame": round(prof["combine_ms"], 4)}
+            if spread is not None:
+                line["ms_per_frame_spread"] = spread
         line["pcie_ms_per_frame"] = pcie_copy_ms(tr)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -185,6 +188,26 @@ def main():
     tr.free()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pass_spread(tr, first_iteration, frames_per_pass, passes=16):
+    """Median / p90 of ms per frame over `passes` separately timed passes (SURVEY §8d asks for
+    median and p90 of frame time).  One sample = one whole multi-frame pass, graph replay and
+    device sync included, divided by its frames: frames of a pass run concurrently, so a single
+    frame has no time of its own.  Runs after the timed region; it is not part of `value`."""
+    f = max(1, int(frames_per_pass))
+    tr.prepare_frames(f)
+    tr.synchronize()
+    samples = []
+    for p in range(passes):
+        t0 = time.perf_counter()
+        tr.trace_frames(first_iteration + p * f, f)
+        tr.synchronize()
+        samples.append(1e3 * (time.perf_counter() - t0) / f)
+    samples.sort()
+    pick = lambda q: samples[min(len(samples) - 1, int(round(q * (len(samples) - 1))))]
+    return {"median": round(pick(0.5), 4), "p90": round(pick(0.9), 4), "passes": passes,
+            "frames_per_pass": f, "note": "each pass timed alone (host wall clock incl. launch + sync)"}
 
 
 def _device_tensor(torch, ptr, n, device):
