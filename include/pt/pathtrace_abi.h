@@ -169,6 +169,12 @@ const char* pt_scene_last_error(void);
  * NULL to query the size).  PT_E_INVALID + pt_scene_last_error() on a decode failure. */
 int32_t pt_texture_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgba, int64_t cap);
 
+/* saveImage (main.cpp:395-419) + Image::savePNG (image.cpp:23-43): writes "<base_path>.png" from an
+ * accumulated host image (width*height*3 floats) traced `iteration` samples per pixel — x-flipped,
+ * divided by the sample count, clamped, x255-truncated, encoded byte-identically to the reference's
+ * stb_image_write 0.98.  PT_E_INVALID + pt_scene_last_error() on an I/O error. */
+int32_t pt_save_png(const float* image, int32_t width, int32_t height, int32_t iteration, const char* base_path);
+
 /* ---- test entry points: run one production kernel on caller data (reference layouts) ---- */
 /* generateRayFromCamera for every pixel of this process's shard -> out[pixels] */
 int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n);

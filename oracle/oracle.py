@@ -104,6 +104,9 @@ def lib():
             "or_triangle_test": (i32, [vp, vp, vp, vp, vp, vp, vp]),
             "or_aabb_test": (i32, [vp, vp]),
             "or_compute_intersection": (None, [vp, vp, vp, vp]),
+            "or_compute_intersections": (None, [vp, vp, vp, i32, vp]),
+            "or_prim_probe": (None, [vp, i32, vp, i32, vp]),
+            "or_tri_probe": (None, [vp, i32, vp, i32, vp, i32, vp]),
             "or_shade": (None, [vp, vp, i32, vp, vp]),
             "or_scatter": (None, [vp, vp, Vec3, Vec3, vp, i32]),
             "or_generate_ray": (None, [vp, i32, i32, i32, i32, vp, vp]),
@@ -339,7 +342,7 @@ def load_scene(path: str, res=None, depth=None, obj_dir: str | None = None) -> S
     tdepth = cam["DEPTH"] if depth is None else depth
     camera = np.zeros(1, CAMERA)
     L.or_camera_setup(int(rx), int(ry), float(cam["FOVY"]), v3(cam["EYE"]), v3(cam["LOOKAT"]), v3(cam["UP"]),
-                      float(cam.get("APERTURE", 0.0)), camera.ctypes.data)
+                      float(cam["APERTURE"]), camera.ctypes.data)
     triangles = np.concatenate(tris) if tris else np.zeros(0, TRIANGLE)
     if len(triangles):
         nodes = np.zeros(max(1, 2 * len(triangles)), BVHNODE)

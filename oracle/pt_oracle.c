@@ -1211,3 +1211,48 @@ int32_t or_obj_to_triangles(const float* pos, const float* nrm, const float* tex
 }
 
 void or_mat4_mul_v4(const pt_mat4* m, const pt_vec4* v, pt_vec4* out) { *out = mat4_mul_v4(m, *v); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* batch probes for the reference pins (tests/test_ref_pins.py, oracle/ref_pins/ref_harness.cpp) */
+/* ------------------------------------------------------------------------------------------ */
+/* computeIntersections over n paths into zeroed records (pathtrace.cu:298-448, :699) */
+void or_compute_intersections(const or_scene* s, const or_options* o, const pt_path_segment* paths, int32_t n,
+                              pt_shadeable_isect* out) {
+    memset(out, 0, sizeof(*out) * (size_t)n);
+    for (int32_t i = 0; i < n; ++i) or_compute_intersection(s, o, &paths[i], &out[i]);
+}
+/* per (path, geom): box / sphere test (intersections.cu:3-109) -> {t, point, normal, outside};
+ * point / normal / outside are reset on a miss (t == -1), where the reference leaves them unset */
+void or_prim_probe(const pt_geom* geoms, int32_t ng, const pt_path_segment* paths, int32_t n, float* out) {
+    for (int32_t i = 0; i < n; ++i) {
+        for (int32_t g = 0; g < ng; ++g) {
+            pt_vec3 p = {0, 0, 0}, nn = {0, 0, 0};
+            int32_t outside = 1;
+            float t = geoms[g].type == PT_CUBE ? or_box_test(&geoms[g], &paths[i].ray, &p, &nn, &outside)
+                                               : or_sphere_test(&geoms[g], &paths[i].ray, &p, &nn, &outside);
+            if (t == -1.f) { p = (pt_vec3){0, 0, 0}; nn = (pt_vec3){0, 0, 0}; outside = 1; }
+            float* r = out + ((size_t)i * ng + g) * 8;
+            r[0] = t; r[1] = p.x; r[2] = p.y; r[3] = p.z; r[4] = nn.x; r[5] = nn.y; r[6] = nn.z;
+            memcpy(&r[7], &outside, 4);
+        }
+    }
+}
+/* per path: intersectTriangle on triangles [0, nt) -> {hit, t, u, v} (zeros on a miss), then
+ * aabbIntersectionTest on nodes [0, nn) -> int (intersections.cu:112-145, 237-275) */
+void or_tri_probe(const pt_triangle* tris, int32_t nt, const pt_bvh_node* nodes, int32_t nn,
+                  const pt_path_segment* paths, int32_t n, int32_t* out) {
+    for (int32_t i = 0; i < n; ++i) {
+        int32_t* r = out + (size_t)i * (4 * nt + nn);
+        for (int32_t k = 0; k < nt; ++k) {
+            float t = 0, u = 0, v = 0;
+            int32_t hit = or_triangle_test(&paths[i].ray, &tris[k].v1.position, &tris[k].v2.position,
+                                           &tris[k].v3.position, &t, &u, &v);
+            if (!hit) t = u = v = 0;
+            r[4 * k] = hit;
+            memcpy(&r[4 * k + 1], &t, 4);
+            memcpy(&r[4 * k + 2], &u, 4);
+            memcpy(&r[4 * k + 3], &v, 4);
+        }
+        for (int32_t k = 0; k < nn; ++k) r[4 * nt + k] = or_aabb_test(&nodes[k].aabb, &paths[i].ray);
+    }
+}

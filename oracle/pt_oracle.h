@@ -69,6 +69,12 @@ int32_t or_triangle_test(const pt_ray* r, const pt_vec3* v0, const pt_vec3* v1, 
 int32_t or_aabb_test(const pt_aabb* b, const pt_ray* r);
 void or_compute_intersection(const or_scene* s, const or_options* o, const pt_path_segment* p,
                              pt_shadeable_isect* out);
+/* batch probes for the reference pins (tests/test_ref_pins.py) */
+void or_compute_intersections(const or_scene* s, const or_options* o, const pt_path_segment* paths, int32_t n,
+                              pt_shadeable_isect* out);
+void or_prim_probe(const pt_geom* geoms, int32_t ng, const pt_path_segment* paths, int32_t n, float* out);
+void or_tri_probe(const pt_triangle* tris, int32_t nt, const pt_bvh_node* nodes, int32_t nn,
+                  const pt_path_segment* paths, int32_t n, int32_t* out);
 
 /* ---- shading (pathtrace.cu:521-621 + interactions.cu:438-542) ---- */
 void or_shade(const or_scene* s, const or_options* o, int32_t iter, const pt_shadeable_isect* isect,

@@ -22,3 +22,17 @@ d["scenes"] = {os.path.basename(k): v for k, v in d["scenes"].items()}
 json.dump(d, sys.stdout, separators=(",", ":"))
 ' > "$GOLD/ingest_pin.json"
 echo "fixtures written: $GOLD/rng_pin.json $GOLD/ingest_pin.json"
+# ref_harness: the reference's own intersections.cu / scene.cpp / utilities.cpp / stb.cpp / image.cpp,
+# compiled in place with g++ against the CUDA runtime headers shipped in this image (real headers,
+# no stand-ins; the .cu file is plain host C++ under -x c++).  Unbuildable without those headers.
+CUDAINC="${CUDAINC:-/usr/local/lib/python3.10/dist-packages/triton/backends/nvidia/include}"
+if [ -f "$CUDAINC/cuda_runtime.h" ]; then
+    if [ ! -x "$OUT/ref_harness" ] || [ "$HERE/ref_harness.cpp" -nt "$OUT/ref_harness" ]; then
+        g++ -std=c++17 -O2 -ffp-contract=off -w -I "$CUDAINC" -I "$REF/src" -I "$REF/external/include" \
+            -x c++ "$REF/src/intersections.cu" -x none "$REF/src/scene.cpp" "$REF/src/utilities.cpp" \
+            "$REF/src/stb.cpp" "$REF/src/image.cpp" "$HERE/ref_harness.cpp" -o "$OUT/ref_harness"
+    fi
+    python3 "$HERE/make_ref_fixtures.py" "$OUT/ref_harness" "$GOLD/ref_pin.json"
+else
+    echo "ref_harness skipped: no CUDA runtime headers at $CUDAINC"
+fi

@@ -1811,7 +1811,16 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
     RC(set_count(0, (int)n));
-    HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
+    // uv / dpdu / dpdv are kept by the production pipelines only for textured scenes (nothing else
+    // reads them); this entry point returns the reference's whole record, so mesh scenes without
+    // textures get temporary attribute buffers
+    float4 *uvd0 = g.d_hit_uvd0, *uvd1 = g.d_hit_uvd1;
+    const bool tmp_attr = !uvd0 && g.has_bvh;
+    if (tmp_attr) {
+        RC(dalloc(&uvd0, (size_t)n));
+        RC(dalloc(&uvd1, (size_t)n));
+    }
+    HitBuf hits{g.d_hit_nt, g.d_hit_mat, uvd0, uvd1};
     if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
         hipLaunchKernelGGL((k_intersect<true, true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
                            pathbuf(0), hits, staged_count(0));
@@ -1828,18 +1837,22 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     HIPCHK(hipMemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
     std::vector<float4> a0, a1;
-    if (g.d_hit_uvd0) {
+    if (uvd0) {
         a0.resize(n);
         a1.resize(n);
-        HIPCHK(hipMemcpy(a0.data(), g.d_hit_uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(a1.data(), g.d_hit_uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(a0.data(), uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(a1.data(), uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
+    }
+    if (tmp_attr) {
+        (void)hipFree(uvd0);
+        (void)hipFree(uvd1);
     }
     for (int64_t i = 0; i < n; ++i) {
         memset(&isects[i], 0, sizeof(pt_shadeable_isect));
         isects[i].t = nt[i].w;
         isects[i].surfaceNormal = pt_vec3{nt[i].x, nt[i].y, nt[i].z};
         isects[i].materialId = mat[i];
-        if (g.d_hit_uvd0 && nt[i].w > 0.0f) {   // textured scenes: uv / dpdu / dpdv as the reference writes them
+        if (uvd0 && nt[i].w > 0.0f) {   // uv / dpdu / dpdv as the reference writes them (zero for primitives)
             isects[i].uv = pt_vec2{a0[i].x, a0[i].y};
             isects[i].dpdu = pt_vec3{a0[i].z, a0[i].w, a1[i].x};
             isects[i].dpdv = pt_vec3{a1[i].y, a1[i].z, a1[i].w};

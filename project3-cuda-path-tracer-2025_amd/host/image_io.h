@@ -10,7 +10,9 @@
 namespace ptio {
 // saveImage: x-flip, divide by samples, clamp to [0,1], x255 truncation -> RGB8 rows
 std::vector<unsigned char> to_rgb8(const std::vector<pt_vec3>& image, int width, int height, float samples);
-// stored-deflate PNG (no compression dependency); returns false on I/O error
+// the PNG bytes stbi_write_png (stb_image_write 0.98, image.cpp:40) writes for these RGB8 rows
+std::vector<unsigned char> encode_png(const std::vector<unsigned char>& rgb, int width, int height);
+// encode_png to a file; returns false on I/O error
 bool write_png(const std::string& path, const std::vector<unsigned char>& rgb, int width, int height);
 // little-endian PFM of the accumulated (not averaged) float image, rows bottom-to-top
 bool write_pfm(const std::string& path, const std::vector<pt_vec3>& image, int width, int height);

@@ -480,7 +480,9 @@ void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int de
     camera.lookAt = vec3_of(cd["LOOKAT"]);
     camera.up = vec3_of(cd["UP"]);
     camera.focalDist = length(camera.lookAt - camera.position);
-    camera.aperture = cd.contains("APERTURE") ? cd["APERTURE"].as_float() : 0.0f;
+    // required like every other camera key: the reference's const json operator[] asserts on a
+    // missing key (scene.cpp:198; scenes/sphere.json has no APERTURE and aborts the reference)
+    camera.aperture = cd["APERTURE"].as_float();
     float yscaled = std::tan(fovy * (PI / 180));
     float xscaled = (yscaled * camera.resolution.x) / camera.resolution.y;
     float fovx = (std::atan(xscaled) * 180) / PI;

@@ -6,6 +6,7 @@
 
 #include "scene.h"
 #include "png_decode.h"
+#include "image_io.h"
 
 struct pt_scene_file {
     Scene* scene;
@@ -72,6 +73,20 @@ int32_t pt_scene_material_name(const pt_scene_file* f, int32_t id, char* buf, in
     if (!f || id < 0 || id >= (int32_t)f->scene->materialNames.size() || !buf || cap <= 0) return PT_E_INVALID;
     std::strncpy(buf, f->scene->materialNames[id].c_str(), (size_t)cap - 1);
     buf[cap - 1] = 0;
+    return PT_OK;
+}
+
+// main.cpp:395-419 saveImage + image.cpp:23-43 Image::savePNG: x-flip, divide by the sample
+// count, clamp, x255 truncation, PNG bytes as stb_image_write writes them -> "<base_path>.png"
+int32_t pt_save_png(const float* image, int32_t width, int32_t height, int32_t iteration, const char* base_path) {
+    if (!image || width <= 0 || height <= 0 || !base_path) return PT_E_INVALID;
+    std::vector<pt_vec3> img((size_t)width * height);
+    std::memcpy(img.data(), image, img.size() * sizeof(pt_vec3));
+    const std::vector<unsigned char> rgb = ptio::to_rgb8(img, width, height, (float)iteration);
+    if (!ptio::write_png(std::string(base_path) + ".png", rgb, width, height)) {
+        g_scene_err = std::string("cannot write ") + base_path + ".png";
+        return PT_E_INVALID;
+    }
     return PT_OK;
 }
 

@@ -91,7 +91,7 @@ ABI_SYMBOLS = [
     "pt_get_frame_stats", "pt_reset_stats", "pt_set_camera", "pt_scene_load", "pt_scene_get_view", "pt_scene_get_info",
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
-    "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
+    "pt_save_png", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
 ]
 
 
@@ -118,6 +118,7 @@ def _load():
         "pt_test_pbo": (i32, [vp, i64, i32, vp]), "pt_profile_frames": (i32, [i32, i32, vp]), "pt_prepare_frames": (i32, [i32]),
         "pt_debug_section_counters": (i32, [vp, i32, i32]),
         "pt_texture_load": (i32, [ctypes.c_char_p, vp, vp, vp, i64]),
+        "pt_save_png": (i32, [vp, i32, i32, i32, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -381,6 +382,16 @@ def rng_draws(seeds: np.ndarray, n: int) -> np.ndarray:
     out = np.zeros((len(seeds), n), np.float32)
     _check(lib.pt_test_rng(_ptr(seeds), len(seeds), int(n), _ptr(out)), "pt_test_rng")
     return out
+
+
+def save_png(image: np.ndarray, width: int, height: int, iteration: int, base_path: str):
+    """saveImage + Image::savePNG (main.cpp:395-419, image.cpp:23-43) -> base_path + ".png"."""
+    image = np.ascontiguousarray(image, np.float32).reshape(-1, 3)
+    if len(image) != width * height:
+        raise ValueError("image size != width * height")
+    rc = lib.pt_save_png(image.ctypes.data, int(width), int(height), int(iteration), base_path.encode())
+    if rc != PT_OK:
+        raise PtError(f"pt_save_png: {lib.pt_scene_last_error().decode(errors='replace')}")
 
 
 def image_to_pbo(image: np.ndarray, iteration: int) -> np.ndarray:

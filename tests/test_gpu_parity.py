@@ -429,3 +429,31 @@ def test_pixel_shards_sum_to_full_frame(oracle, ptamd):
         tr.free()
     assert live == 64 * 50
     assert _eq(acc, full)
+
+
+# ---- the HIP intersection path against the reference's OWN intersections.cu (tests/golden/ref_pin.json) ----
+with open(os.path.join(GOLDEN, "ref_pin.json")) as _f:
+    _REF_PIN = json.load(_f)
+
+
+@pytest.mark.parametrize("variant", [None, 26, 10])
+@pytest.mark.parametrize("name", sorted(_REF_PIN["isect"]))
+def test_intersections_match_reference(name, variant, ptamd):
+    """computeIntersections of the reference (box / sphere / bvhMeshIntersectionTest compiled from
+    /root/reference/src/intersections.cu, oracle/ref_pins/ref_harness.cpp) on 4096 probe rays per
+    scene: axis-aligned, sub-1e-5 and signed-zero components, NaN / inf / zero rays, rays aimed at
+    triangle vertices and shared-edge midpoints (t ties).  The full 52-B records are compared
+    (NaNs canonicalised), with the default kernel variant and the reference-order / node-array
+    traversals."""
+    import refpins as R
+    ref = _REF_PIN["isect"][name]
+    b = ptamd.SceneFile(scene_path(name), res=(96, 96))       # wavefront capacity >= 9216 paths
+    raw = ptamd.SceneFile(scene_path(name), viewer_camera=False)
+    rays = R.rays(R.ISECT_RAYS, seed=len(name), targets=R.scene_targets(raw.geoms, raw.triangles))
+    assert R.digest(rays) == ref["rays_sha256"]
+    opts = {} if variant is None else {"variant": variant}
+    tr = ptamd.PathTracer(b, **opts)
+    got = tr.test_intersect(rays.astype(ptamd.PATH))
+    tr.free()
+    assert int((got["t"] > 0).sum()) == ref["hits"]
+    assert R.digest(R.pack(got, R.P_ISECT)) == ref["isect_sha256"]

@@ -151,3 +151,17 @@ def test_known_answer_first_nan_pixel(oracle):
     r.trace(8)
     bad = np.where(~np.isfinite(r.image).all(axis=1))[0]
     assert bad.tolist() == [406300]
+
+
+def test_known_answer_config1_live_counts(oracle):
+    """SURVEY §8a config 1 (cornell 400x400 depth 4): 160000, 130706, 90064, 69475, Σ 450,244.
+    These are the per-bounce MEANS over iterations 1-4 (130705.5 rounds to 130706; the sum of the
+    unrounded means is 450244.5), i.e. the counts of SURVEY's 4-spp timing run — not one
+    iteration's.  Exhaustive search over windows of iterations 1..200, both vec2 argument orders
+    and depths 4 / 5 / 8 finds only this window (round-1 VERDICT "What's weak" 1)."""
+    sc = oracle.load_scene(scene_path("cornell"), res=(400, 400), depth=4)
+    r = oracle.Renderer(sc, oracle.options(trig_mode=0, arg_order=0))
+    rows = np.array([r.trace(it) for it in range(1, 5)], np.float64)
+    m = rows.mean(axis=0)
+    assert m.tolist() == [160000.0, 130705.5, 90064.0, 69475.0]
+    assert int(m.sum()) == 450244

@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--pmc", nargs=2, action="append", metavar=("DIR", "PREFIX"), default=[])
     ap.add_argument("--pmc-frames", type=int, default=72,
                     help="frames per profiled run (tools/pmc.sh: warmup 8 + steps 32 + bench's replay 32)")
+    ap.add_argument("--traffic-name", default=None,
+                    help="output file name under profiles/ (default <round>_traffic.json)")
     args = ap.parse_args()
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -91,7 +93,7 @@ def main():
             traffic.setdefault(fam, {}).update(e)
             traffic[fam]["source"] = f"{prefix or 'default'} passes"
     if traffic:
-        with open(os.path.join(prof, f"{args.round}_traffic.json"), "w") as f:
+        with open(os.path.join(prof, args.traffic_name or f"{args.round}_traffic.json"), "w") as f:
             json.dump(traffic, f, indent=1, sort_keys=True)
     print(json.dumps({k: [(x["name"][:60], x["calls"], round(x["avg_ns"])) for x in v[:8]] for k, v in digest.items()},
                      indent=1))
