@@ -1,29 +1,40 @@
 """bench.py — BASELINE.json's headline: Mpaths/s (path segments traced per second) and ms/frame
 for scenes/cornell.json at 800x800, depth 8, stream compaction on (BASELINE configs[1]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--pipeline fused|staged] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pipeline fused|staged]
+                    [--shard pixels|samples] [--no-cpu-baseline] [--no-configs]
 
-A "step" is one pathtrace() frame: one sample for every pixel, all bounces, accumulated into the
-HBM-resident image (no host copy: pathtrace.cu's per-frame 7.68 MB D->H copy is outside `value`,
-its cost is reported separately as `pcie_ms_per_frame`).  With N > 1 (launched by
-torch.distributed.run, one rank per GPU) every rank traces full frames with its own iteration
-numbers (sample sharding, weak scaling: rank r traces a contiguous block of iterations), and the
-accumulated framebuffers are summed to rank 0 with one RCCL reduce inside the timed region.
+A "step" is one pathtrace() frame's worth of work per GPU: one sample for every pixel, all
+bounces, accumulated into the HBM-resident image (the reference's per-frame 7.68 MB D->H copy is
+outside `value`; the API-faithful single-frame time including it is `api`).
 
-Timing: W untimed frames, then barrier + device sync, K frames, device sync + barrier; the MAX over
+N GPUs: one process per GPU.  `python bench.py --gpus N` without WORLD_SIZE starts
+`torch.distributed.run --nproc-per-node N` as a child process (before touching any GPU) and exits
+with its code; under torchrun WORLD_SIZE must equal --gpus.  Default sharding is by PIXEL TILE
+(the north star's partition): rank r traces the interleaved row bands
+(y // rows) % N == r of every frame, for N x K frames, so per-GPU work is K frames' worth of
+paths (weak scaling) and the whole job is N x K samples per pixel.  The only exchange is one
+gather of the ranks' disjoint tiles into rank 0's framebuffer (RCCL over xGMI), inside the timed
+region; the result is bit-identical to one GPU tracing the same N x K frames.  `--shard samples`
+instead gives each rank whole frames (a contiguous block of iterations) and sums the full
+framebuffers with one RCCL reduce.
+
+Timing: W untimed frames, then barrier + device sync, K steps, device sync + barrier; the MAX over
 ranks of the elapsed time; value = segments traced by all ranks / that time.  The timed frames run
 as the library runs them: one hipGraph per multi-frame pass, replayed back to back.  On one GPU the
-same number of frames is then replayed once more, launched eagerly with HIP start/stop events on
-every kernel (hipExtLaunchKernel, on the library's stream); that replay gives the dominant kernel's
-average duration for the `roofline` object (algorithmic bytes / duration).  It is kept out of the
-timed region because per-dispatch timestamps cost ~7 % of frame time between kernels.
-Everything traced is the real workload: the cornell scene from the reference's JSON, no work
-skipped.  rank 0 then times the CPU oracle (oracle/, a port of the reference path with
-stream_compaction/cpu.cu's compactWithScan) on a bounded sample for `cpu_baseline`.
+same frames are then replayed eagerly with HIP start/stop events on every kernel
+(hipExtLaunchKernel, on the library's stream): the dominant kernel's average launch duration for
+`roofline` (algorithmic bytes / duration).  Then, still on one GPU: `api` times single
+pt_trace() calls as main.cpp:463 makes them (F = 1, image copied to host memory every frame),
+`configs` adds BASELINE configs[2..4] as sub-records (own workload string and roofline each), and
+rank 0 times the CPU oracle (oracle/, the port of the reference path with stream_compaction/cpu.cu's
+compactWithScan) on a bounded sample for `cpu_baseline`.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,6 +48,15 @@ REF_MS_PER_FRAME = 42.204      # reference README.md:136, RTX 3060 Laptop, compa
 STATE_BYTES = 48               # one path in flight: 3 x float4 (origin|pixel, dir|bounces, rgb|-)
 IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3 (1-frame pass)
 PLANE_STORE_BYTES = 12         # terminated path of an F-frame pass: float3 store to its frame's plane
+N_CUS = 256                    # MI355X compute units
+
+# BASELINE.json configs[2..4] as sub-records of the N=1 line: (tag, scene, res, depth, sort, pipeline, steps, warmup)
+SUB_CONFIGS = [
+    ("configs[2]", "cornell_glass_test.json", None, None, True, "staged", 48, 4),
+    ("configs[2] fused", "cornell_glass_test.json", None, None, False, "fused", 64, 8),
+    ("configs[3]", "cornell_obj_bnnuy.json", None, None, False, "fused", 48, 4),
+    ("configs[4]", "cornell_obj_khaslana.json", (1600, 1600), 12, False, "fused", 16, 2),
+]
 
 
 def parse():
@@ -50,21 +70,50 @@ def parse():
     ap.add_argument("--res", default="", help="WxH override (configs[4]: 1600x1600)")
     ap.add_argument("--depth", type=int, default=-1, help="trace depth override (configs[4]: 12)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the configs[2..4] sub-records")
+    ap.add_argument("--no-api", action="store_true", help="skip the single-frame pt_trace() timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--shard", choices=["samples", "pixels"], default="samples",
-                    help="N>1: samples = every rank traces whole frames (weak scaling); pixels = each "
-                         "frame's interleaved row bands split over the ranks (strong scaling)")
+    ap.add_argument("--shard", choices=["pixels", "samples"], default="pixels",
+                    help="N>1: pixels = interleaved row bands of every frame per rank (default); "
+                         "samples = whole frames per rank")
+    ap.add_argument("--dump-image", default="", help="rank 0 saves the final accumulated image (.npy)")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: run torch.distributed.run as a CHILD process (never an exec,
+    and before this process touches any GPU), one rank per GPU, and return its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def shard_rows(height: int, world: int) -> int:
+    """Row-band height: the largest of 8/4/2/1 that splits the image evenly over the ranks."""
+    for rows in (8, 4, 2, 1):
+        if height % (rows * world) == 0:
+            return rows
+    return 1
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     import torch                     # first: ptamd then shares torch's HIP runtime
     import torch.distributed as dist
     sys.path.insert(0, PKG)
     import ptamd
+    from ptamd import dist as pdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RCCL (backend "nccl") in production; PT_BENCH_BACKEND=gloo rehearses the multi-rank logic
@@ -81,21 +130,25 @@ def main():
     res = tuple(int(x) for x in args.res.split("x")) if args.res else None
     scene = ptamd.SceneFile(args.scene, res=res, depth=args.depth if args.depth >= 0 else None)
     pipeline = ptamd.PIPELINE_STAGED if args.pipeline == "staged" else ptamd.PIPELINE_FUSED
-    shard = {}
-    if world > 1 and args.shard == "pixels":
-        shard = dict(shard_mode=ptamd.SHARD_PIXELS, shard_rank=rank, shard_count=world, shard_rows=8)
+    pixels = world > 1 and args.shard == "pixels"
+    rows = shard_rows(scene.height, world) if pixels else 8
+    shard = dict(shard_mode=ptamd.SHARD_PIXELS, shard_rank=rank, shard_count=world, shard_rows=rows) if pixels else {}
     tr = ptamd.PathTracer(scene, device=device, pipeline=pipeline, material_sort=int(args.sort), **shard)
     depth = scene.trace_depth
 
-    # SAMPLES sharding: rank r traces the contiguous iteration block 1 + r*(W+K) .. (r+1)*(W+K)
-    # (ptamd.dist.sample_iterations), so its frames group into multi-frame passes.  PIXELS: every
-    # rank traces iterations 1.. for its own row bands.
-    it = 1 + (rank * (args.warmup + args.steps) if not shard else 0)
+    # iterations: PIXELS -- every rank traces iterations 1..N(W+K) over its own tiles (N frames per
+    # step); SAMPLES -- rank r traces the contiguous block 1 + r(W+K) .. (r+1)(W+K)
+    per_step = world if pixels else 1
+    it = 1 + (0 if pixels else rank * (args.warmup + args.steps))
     if args.warmup:
-        tr.trace_frames(it, args.warmup)
-        it += args.warmup
+        tr.trace_frames(it, args.warmup * per_step)
+        it += args.warmup * per_step
     tr.synchronize()
     tr.reset_stats()
+    combiner = None
+    if world > 1:
+        combiner = (pdist.TileGather(tr, rows, world, rank, backend, device) if pixels
+                    else pdist.ImageReduce(tr, rank, backend, device))
 
     def barrier():
         if world > 1:
@@ -103,53 +156,54 @@ def main():
         torch.cuda.synchronize()      # same HIP runtime as the library: covers its stream too
         tr.synchronize()
 
-    tr.prepare_frames(args.steps)                      # capture the pass graphs now, not while timed
+    tr.prepare_frames(args.steps * per_step)           # capture the pass graphs now, not while timed
     barrier()
     t0 = time.perf_counter()
-    tr.trace_frames(it, args.steps)                    # K frames: the pass graphs, back to back
-    tr.synchronize()
-    if world > 1:
-        if backend == "nccl":
-            ptr, n = tr.image_device_ptr()
-            img = _device_tensor(torch, ptr, n, device)
-        else:
-            img = torch.from_numpy(tr.image().reshape(-1))
-        dist.reduce(img, dst=0, op=dist.ReduceOp.SUM)   # one framebuffer combine (RCCL over xGMI)
-        torch.cuda.synchronize()
+    tr.trace_frames(it, args.steps * per_step)         # K steps: the pass graphs, back to back
+    t_comb = 0.0
+    if combiner is not None:
+        tr.synchronize()
+        tc = time.perf_counter()
+        combiner.run()                                 # one framebuffer combine (RCCL over xGMI)
+        t_comb = time.perf_counter() - tc
     tr.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    it += args.steps * per_step
 
     st = tr.stats()
     segs = st["segments_total"]
-    frames = st["frames_total"]
-    assert frames == args.steps, (frames, args.steps)
-    prof = st_prof = None
+    assert st["frames_total"] == args.steps * per_step, (st["frames_total"], args.steps, per_step)
+    if args.dump_image and rank == 0:
+        np.save(args.dump_image, tr.image())
+    prof = st_prof = spread = None
     if world == 1:
         # kernel durations: the next K frames replayed eagerly with events around every kernel
         tr.reset_stats()
-        prof = tr.profile(it + args.steps, args.steps)
+        prof = tr.profile(it, args.steps)
         st_prof = tr.stats()
-        spread = pass_spread(tr, it + 2 * args.steps, st_prof["frames_per_pass"])
+        spread = pass_spread(tr, it + args.steps, st_prof["frames_per_pass"])
+    seen_world = world
     if world > 1:
-        t = torch.tensor([elapsed, float(segs)], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, float(segs), t_comb], dtype=torch.float64,
+                         device="cuda" if backend == "nccl" else "cpu")
         tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, segs = float(tmax[0]), float(t[1])
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, segs, t_comb = float(tmax[0]), float(t[1]), float(tmax[2])
+        seen_world = dist.get_world_size()
     ms_per_step = 1e3 * elapsed / args.steps
     value = segs / elapsed / 1e6
 
     if rank == 0:
         headline = (os.path.abspath(args.scene) == SCENE and not args.res and args.depth < 0 and not args.sort)
         name = os.path.basename(args.scene)
-        if args.sort and args.pipeline == "fused":
-            sort = ("material sort requested: the fused pipeline shades each path in registers right after "
-                    "its intersection, so there is nothing to sort (results are order-independent); "
-                    "--pipeline staged runs the sort")
+        workload = workload_str(name, tr.width, tr.height, depth, args.sort, args.pipeline)
+        if world > 1:
+            par = (f"pixel tiles x{world}: interleaved {rows}-row bands, {world} frames per step, tile gather "
+                   f"to rank 0" if pixels else f"samples x{world}: whole frames per rank, framebuffer reduce")
         else:
-            sort = f"sort {'on' if args.sort else 'off'}"
-        workload = f"{name} {tr.width}x{tr.height} depth {depth}, stream compaction on, {sort}"
+            par = "single GPU"
         line = {
             "metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8" if headline
                       else f"Mpaths/s (rays x bounces / s), {workload}",
@@ -160,34 +214,99 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong" if shard else "weak",
-            "vs_baseline": round(REF_MS_PER_FRAME / ms_per_step, 2) if headline else None,
-            "vs_baseline_basis": "reference ms/frame 42.204 (README.md:136, RTX 3060 Laptop) / our ms_per_step"
+            "scaling": "weak",
+            "vs_baseline": round(REF_MS_PER_FRAME / (ms_per_step / per_step), 2) if headline else None,
+            "vs_baseline_basis": "reference ms/frame 42.204 (README.md:136, RTX 3060 Laptop) / our ms per frame"
                                  if headline else "no published reference number for this workload",
             "dtype": "f32",
-            "data": f"scenes/{name} from the reference ({tr.width}x{tr.height}, depth {depth}, 1 spp per step)"
+            "data": f"scenes/{name} from the reference ({tr.width}x{tr.height}, depth {depth}, 1 spp per frame)"
                     + ("; synthetic stand-in meshes (reference OBJs absent)" if "obj" in name else
                        "; no synthetic inputs"),
             "config": {"workload": workload + (" (BASELINE configs[1])" if headline else ""),
-                       "pipeline": args.pipeline, "segments_per_frame": round(segs / args.steps / (1 if shard else world), 1),
-                       "frames_per_pass": st["frames_per_pass"],
-                       "parallelism": (f"{args.shard}-sharded x{world}" if world > 1 else "single GPU")},
+                       "pipeline": args.pipeline,
+                       "segments_per_frame": round(segs / (args.steps * per_step) / (1 if pixels else world), 1),
+                       "frames_per_pass": st["frames_per_pass"], "parallelism": par},
         }
+        if world > 1:
+            line["distributed"] = {"world_size": seen_world, "backend": "rccl" if backend == "nccl" else backend,
+                                   "shard": args.shard, "frames_per_step": per_step,
+                                   "combine_ms": round(1e3 * t_comb, 3),
+                                   "combine": "gather of disjoint row-band tiles" if pixels else "reduce(SUM)"}
         if prof is not None:
-            line["roofline"] = roofline(prof, st_prof, args, depth, headline)
-            line["kernels"] = {"frame_ms": round(prof["frame_ms"], 4), "passes": prof["passes"],
-                               "per_launch_bounce_ms": [round(x, 4) for x in prof["bounce_ms"]],
-                               "per_launch_bvh_ms": [round(x, 4) for x in prof["bvh_ms"]],
-                               "combine_ms_per_frame": round(prof["combine_ms"], 4)}
-            if spread is not None:
-                line["ms_per_frame_spread"] = spread
+            line["roofline"] = roofline(prof, st_prof, args.pipeline, args.steps, depth, headline)
+            line["kernels"] = kernels_digest(prof, spread)
         line["pcie_ms_per_frame"] = pcie_copy_ms(tr)
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+        if world == 1 and not args.no_api:
+            line["api"] = api_frame_ms(tr, it + 3 * args.steps)
     tr.free()
+    if rank == 0 and world == 1:
+        if not args.no_configs:
+            line["configs"] = [sub_config(ptamd, c) for c in SUB_CONFIGS]
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def workload_str(name, w, h, depth, sort, pipeline):
+    if sort and pipeline == "fused":
+        s = ("material sort requested: the fused pipeline shades each path in registers right after its "
+             "intersection, so there is nothing to sort (results are order-independent); --pipeline staged runs it")
+    else:
+        s = f"sort {'on' if sort else 'off'}"
+    return f"{name} {w}x{h} depth {depth}, stream compaction on, {s}"
+
+
+def kernels_digest(prof, spread):
+    d = {"frame_ms": round(prof["frame_ms"], 4), "passes": prof["passes"],
+         "per_launch_bounce_ms": [round(x, 4) for x in prof["bounce_ms"]],
+         "per_launch_bvh_ms": [round(x, 4) for x in prof["bvh_ms"]],
+         "combine_ms_per_frame": round(prof["combine_ms"], 4)}
+    if spread is not None:
+        d["ms_per_frame_spread"] = spread
+    return d
+
+
+def sub_config(ptamd, cfg):
+    """One BASELINE config on this GPU: warmup, K timed frames (pass graphs), eager profiled
+    replay for its roofline.  Same timing rules as the headline."""
+    tag, scene_name, res, depth, sort, pipeline, steps, warmup = cfg
+    path = os.path.join(REPO, "scenes", scene_name)
+    sc = ptamd.SceneFile(path, res=res, depth=depth)
+    tr = ptamd.PathTracer(sc, pipeline=ptamd.PIPELINE_STAGED if pipeline == "staged" else ptamd.PIPELINE_FUSED,
+                          material_sort=int(sort))
+    it = 1
+    tr.trace_frames(it, warmup)
+    it += warmup
+    tr.synchronize()
+    tr.reset_stats()
+    tr.prepare_frames(steps)
+    tr.synchronize()
+    t0 = time.perf_counter()
+    tr.trace_frames(it, steps)
+    tr.synchronize()
+    el = time.perf_counter() - t0
+    it += steps
+    st = tr.stats()
+    tr.reset_stats()
+    prof = tr.profile(it, steps)
+    st_prof = tr.stats()
+    d = sc.trace_depth
+    out = {"config": tag, "workload": workload_str(scene_name, tr.width, tr.height, d, sort, pipeline),
+           "pipeline": pipeline, "steps": steps, "warmup": warmup,
+           "ms_per_frame": round(1e3 * el / steps, 4),
+           "value": round(st["segments_total"] / el / 1e6, 2), "unit": "Mpaths/s",
+           "segments_per_frame": round(st["segments_total"] / steps, 1), "frames_per_pass": st["frames_per_pass"],
+           "data": "synthetic stand-in meshes (reference OBJs absent)" if "obj" in scene_name else "reference scene",
+           "roofline": roofline(prof, st_prof, pipeline, steps, d, False),
+           "kernels": kernels_digest(prof, None)}
+    if tag == "configs[4]":
+        out["note"] = "BASELINE names 8 GPUs for this config; this sub-record is one GPU (bench.py --gpus 8 --scene ...)"
+    tr.free()
+    sc.close()
+    return out
 
 
 def pass_spread(tr, first_iteration, frames_per_pass, passes=16):
@@ -205,9 +324,31 @@ def pass_spread(tr, first_iteration, frames_per_pass, passes=16):
         tr.synchronize()
         samples.append(1e3 * (time.perf_counter() - t0) / f)
     samples.sort()
-    pick = lambda q: samples[min(len(samples) - 1, int(round(q * (len(samples) - 1))))]
+    pick = lambda q: samples[min(len(samples) - 1, int(round(q * (len(samples) - 1))))]  # noqa: E731
     return {"median": round(pick(0.5), 4), "p90": round(pick(0.9), 4), "passes": passes,
             "frames_per_pass": f, "note": "each pass timed alone (host wall clock incl. launch + sync)"}
+
+
+def api_frame_ms(tr, first_iteration, frames=40, warm=5):
+    """API-faithful frame: pathtrace(pbo, 0, iter) as main.cpp:463 calls it -- one
+    frame per call (F = 1), the accumulated image copied into host memory every call
+    (pathtrace.cu:783; the library page-locks the caller's buffer once) -- median / p90 of the
+    host wall time per call, with and without that copy."""
+    def run(copy, first):
+        ts = []
+        for k in range(warm + frames):
+            t0 = time.perf_counter()
+            tr.trace(first + k, copy_image=copy)
+            if not copy:
+                tr.synchronize()
+            if k >= warm:
+                ts.append(1e3 * (time.perf_counter() - t0))
+        ts.sort()
+        return round(ts[len(ts) // 2], 4), round(ts[int(0.9 * (len(ts) - 1))], 4)
+    m_copy, p_copy = run(True, first_iteration)
+    m_nc, p_nc = run(False, first_iteration + warm + frames)
+    return {"ms_per_frame": m_copy, "p90": p_copy, "ms_per_frame_no_copy": m_nc, "p90_no_copy": p_nc,
+            "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into page-locked host memory per call"}
 
 
 def _device_tensor(torch, ptr, n, device):
@@ -217,7 +358,7 @@ def _device_tensor(torch, ptr, n, device):
     return torch.as_tensor(_Cai(), device=f"cuda:{device}")
 
 
-def roofline(prof, st, args, depth, headline=True):
+def roofline(prof, st, pipeline, steps, depth, headline=True):
     """Dominant kernel, per launch.  Fused: the bounce kernel (camera|intersect|shade|gather|
     compact; `depth` launches per pass of F frames): algorithmic bytes = 48 B per path read
     (bounce > 0) + 48 B per survivor written + 24 B image read-modify-write (or 12 B plane store)
@@ -229,15 +370,15 @@ def roofline(prof, st, args, depth, headline=True):
     nbytes = 0
     for b in range(depth):
         n_in, n_out = tot[b], tot[b + 1] if b + 1 < len(tot) else 0
-        if args.pipeline == "fused":
+        if pipeline == "fused":
             gather = IMAGE_RMW_BYTES if st["frames_per_pass"] == 1 else PLANE_STORE_BYTES
             nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + gather * (n_in - n_out)
         else:
             nbytes += 4 * n_in + 2 * STATE_BYTES * n_out
-    if args.pipeline == "fused" and any(prof["bvh_ms"][:depth]):
+    if pipeline == "fused" and any(prof["bvh_ms"][:depth]):
         name = ("k_bounce + k_bvh_bounce (fused bounce; mesh rays traversed and shaded by the second "
                 "kernel), one pair of launches per bounce per pass")
-    elif args.pipeline == "fused":
+    elif pipeline == "fused":
         name = "k_bounce (fused camera|intersect|shade|gather|compact, one launch per bounce per pass)"
     else:
         name = "k_compact_scatter (stable partition: flags + survivor payload move)"
@@ -246,7 +387,7 @@ def roofline(prof, st, args, depth, headline=True):
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     pmc = _pmc(name) if headline else {}     # the committed PMC pass is of the headline run
     # measured HBM bytes per launch: the PMC run's bytes per frame x this run's frames per launch
-    traffic = (int(pmc["hbm_bytes_per_frame"] * args.steps / launches) if pmc.get("hbm_bytes_per_frame")
+    traffic = (int(pmc["hbm_bytes_per_frame"] * steps / launches) if pmc.get("hbm_bytes_per_frame")
                else pmc.get("hbm_bytes_per_launch"))
     line = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -260,17 +401,21 @@ def roofline(prof, st, args, depth, headline=True):
         clk = pmc["GRBM_GUI_ACTIVE"] / 8.0
         rate = pmc["SQ_INSTS_VALU"] / (clk * N_CUS)
         line["valu_issue"] = {"achieved": round(rate, 3), "peak": 2.0, "unit": "wave64 VALU instr / CU / clk",
-                              "frac": round(rate / 2.0, 3), "source": "profiles/r01_traffic.json (rocprofv3 PMC)"}
+                              "frac": round(rate / 2.0, 3), "source": f"profiles/{_pmc_file()} (rocprofv3 PMC)"}
     return line
 
 
-N_CUS = 256      # MI355X compute units
+def _pmc_file():
+    """The newest committed PMC digest of the headline run (profiles/rNN_traffic.json)."""
+    d = os.path.join(REPO, "profiles")
+    names = sorted(f for f in os.listdir(d) if f.endswith("_traffic.json") and f[1:3].isdigit()) if os.path.isdir(d) else []
+    return names[-1] if names else "r01_traffic.json"
 
 
 def _pmc(name):
-    """The kernel's per-launch PMC digest from the committed rocprofv3 pass (profiles/r01_traffic.json):
-    HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) and counters."""
-    p = os.path.join(REPO, "profiles", "r01_traffic.json")
+    """The kernel's per-launch PMC digest from the committed rocprofv3 pass: HBM bytes
+    (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) and counters."""
+    p = os.path.join(REPO, "profiles", _pmc_file())
     if not os.path.exists(p):
         return {}
     with open(p) as f:
@@ -281,7 +426,7 @@ def _pmc(name):
 
 def pcie_copy_ms(tr):
     """The reference copies the accumulated image to the host every frame (pathtrace.cu:783):
-    time one such copy."""
+    time one such copy into fresh pageable memory (the `api` record uses page-locked memory)."""
     tr.synchronize()
     t0 = time.perf_counter()
     for _ in range(5):

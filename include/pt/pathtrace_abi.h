@@ -124,7 +124,10 @@ int32_t pt_free(void);
  * 1-based `iteration`, add it into the accumulated image, write the 8-bit preview into
  * `pbo_device` (a DEVICE pointer of width*height pt_uchar4, or NULL), and copy the
  * accumulated (not averaged) image into `host_image` (width*height*3 floats, or NULL) —
- * the reference copies into scene->state.image every call (pathtrace.cu:783-784). */
+ * the reference copies into scene->state.image every call (pathtrace.cu:783-784).  The library
+ * page-locks `host_image` (hipHostRegister) on first use so the copy runs at PCIe rate; like
+ * state.image it must stay the same live allocation across calls — passing a different pointer
+ * re-registers, pt_free releases it. */
 int32_t pt_trace(pt_uchar4* pbo_device, int32_t frame, int32_t iteration, float* host_image);
 
 /* Trace `count` frames with iterations first_iteration .. first_iteration+count-1, image stays

@@ -36,3 +36,14 @@ if [ -f "$CUDAINC/cuda_runtime.h" ]; then
 else
     echo "ref_harness skipped: no CUDA runtime headers at $CUDAINC"
 fi
+# dropin_main: a main.cpp-shaped caller compiled against the reference's own headers and host
+# sources (Scene from scene.cpp) + the drop-in (project3-cuda-path-tracer-2025_amd/dropin/pathtrace.cpp),
+# linked against libptamd.so -- proves the drop-in links behind main.cpp's calls
+PKGDIR="$REPO/project3-cuda-path-tracer-2025_amd"
+if [ -f "$CUDAINC/cuda_runtime.h" ] && [ -f "$PKGDIR/build/libptamd.so" ]; then
+    g++ -std=c++17 -O2 -ffp-contract=off -w -I "$CUDAINC" -I "$REF/src" -I "$REF/external/include" -I "$REPO/include" \
+        "$HERE/dropin_main.cpp" "$PKGDIR/dropin/pathtrace.cpp" "$REF/src/scene.cpp" "$REF/src/utilities.cpp" \
+        "$REF/src/stb.cpp" -L "$PKGDIR/build" -lptamd -Wl,-rpath,'$ORIGIN/../../project3-cuda-path-tracer-2025_amd/build' \
+        -o "$OUT/dropin_main"
+    echo "drop-in caller built: $OUT/dropin_main"
+fi

@@ -12,8 +12,9 @@
 //
 //  STAGED: one kernel per reference stage — camera, intersect, [material sort], shade,
 //    compaction — each a separately testable HIP kernel.  Its compaction is a STABLE
-//    single-pass partition (wave ballot/mbcnt block scan + decoupled look-back across tiles),
-//    the drop-in for thrust::stable_partition(PathAlive) (pathtrace.cu:750-757).
+//    partition in three order-independent launches — per-tile alive counts, one single-
+//    workgroup scan of the tile counts, scatter (wave ballot/mbcnt within a tile) — the drop-in
+//    for thrust::stable_partition(PathAlive) (pathtrace.cu:750-757).
 //
 // A frame is captured once into a hipGraph and replayed; the iteration number lives in
 // device memory (k_frame_begin advances it), so the replay needs no parameter updates.
@@ -781,6 +782,10 @@ struct State {
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
     int key_bits = 1;
+    // pt_trace's host image (the reference's scene->state.image): page-locked with hipHostRegister
+    // on first use so the per-frame D->H copy (pathtrace.cu:783) runs at full PCIe rate
+    void* host_reg = nullptr;
+    size_t host_reg_bytes = 0;
 };
 State g;
 
@@ -1010,6 +1015,27 @@ int bvh_max_stack(const pt_bvh_node* nodes, int n) {
     return (int)mx;
 }
 
+// levels of the tree below node 0 (root = 1); -1 for a malformed tree (a child out of range or
+// reached twice).  The near-first traversals (VAR_BVH_FAST) push at most one entry per level.
+int bvh_height(const pt_bvh_node* nodes, int n) {
+    if (n <= 0) return 0;
+    std::vector<std::pair<int, int>> st{{0, 1}};
+    std::vector<char> seen(n, 0);
+    int h = 0;
+    while (!st.empty()) {
+        const int i = st.back().first, d = st.back().second;
+        st.pop_back();
+        if (i < 0 || i >= n || seen[i]) return -1;
+        seen[i] = 1;
+        h = std::max(h, d);
+        const pt_bvh_node& nd = nodes[i];
+        if (nd.triCount > 0 && nd.start >= 0) continue;
+        if (nd.left >= 0) st.push_back({nd.left, d + 1});
+        if (nd.right >= 0) st.push_back({nd.right, d + 1});
+    }
+    return h;
+}
+
 void free_all() {
     release_graph();
     void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
@@ -1021,6 +1047,7 @@ void free_all() {
         for (int k = 0; k < 3; ++k)
             if (g.d_path[i][k]) (void)hipFree(g.d_path[i][k]);
     if (g.stream) (void)hipStreamDestroy(g.stream);
+    if (g.host_reg) (void)hipHostUnregister(g.host_reg);
     int32_t* td = g.traced_depth;
     g = State();
     g.traced_depth = td;
@@ -1446,7 +1473,22 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             c.dpdv[0] = t.dpdv.x; c.dpdv[1] = t.dpdv.y; c.dpdv[2] = t.dpdv.z;
             c.materialID = t.materialID;
         }
-        g.stack_depth = std::min(MAXSTACK, std::max(2, bvh_max_stack(s->bvh_nodes, s->num_bvh_nodes)));
+        // traversal stack (LDS, MAXSTACK entries per lane at most).  The reference-order DFS needs
+        // bvh_max_stack entries -- more than 64 overflows the reference's own int stack[64]
+        // (intersections.cu:167), so such a tree is refused rather than traversed differently.
+        // The near-first traversals need up to height + 1; a tree too deep (or malformed) for
+        // that keeps the reference-order traversal.  No push is ever dropped.
+        const int ref_stack = bvh_max_stack(s->bvh_nodes, s->num_bvh_nodes);
+        if (ref_stack > MAXSTACK)
+            return fail(PT_E_UNSUPPORTED, "BVH needs a %d-entry traversal stack; the reference's holds %d "
+                        "(intersections.cu:167)", ref_stack, MAXSTACK);
+        const int tree_height = bvh_height(s->bvh_nodes, s->num_bvh_nodes);
+        if (tree_height < 0 || tree_height + 1 > MAXSTACK) {
+            o.variant &= ~(VAR_BVH_FAST | VAR_BVH_SPLIT);
+            g.opts.variant = o.variant;
+        }
+        g.stack_depth = std::max(2, ref_stack);
+        if (o.variant & VAR_BVH_FAST) g.stack_depth = std::max(g.stack_depth, tree_height + 1);
         // VAR_BVH_FAST pair layout (DevPair): walk the tree in the reference's visit order
         // (push left, push right, pop -> right subtree first), numbering internal nodes (pairs)
         // and leaves (4-slot triangle groups).  Any tree this layout cannot hold exactly -- a
@@ -1536,7 +1578,6 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;
-                g.stack_depth = std::max(g.stack_depth, std::min(MAXSTACK, height + 1));
             }
         }
         g.bvh_lds = (size_t)g.stack_depth * BLOCK * sizeof(int);
@@ -1688,11 +1729,40 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
                            g.pixels_total, iteration);
         HIPCHK(hipGetLastError());
     }
-    if (host_image)
-        HIPCHK(hipMemcpyAsync(host_image, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total,
-                              hipMemcpyDeviceToHost, g.stream));
+    if (host_image) {
+        const size_t bytes = sizeof(float) * 3 * (size_t)g.pixels_total;
+        if (g.host_reg != host_image || g.host_reg_bytes != bytes) {
+            if (g.host_reg) (void)hipHostUnregister(g.host_reg);
+            g.host_reg = nullptr;
+            // pageable memory the caller owns; when it cannot be registered the copy still works
+            if (hipHostRegister(host_image, bytes, hipHostRegisterDefault) == hipSuccess) {
+                g.host_reg = host_image;
+                g.host_reg_bytes = bytes;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
+        HIPCHK(hipMemcpyAsync(host_image, g.d_image, bytes, hipMemcpyDeviceToHost, g.stream));
+    }
     HIPCHK(hipStreamSynchronize(g.stream));
-    if (g.traced_depth) *g.traced_depth = std::max(1, g.sc.trace_depth);
+    if (g.traced_depth) {
+        // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770): the
+        // loop stops after bounce k when no path is left alive, or at traceDepth
+        int depth = std::max(1, g.sc.trace_depth);
+        if (g.opts.stream_compaction) {
+            std::vector<int> cnt((size_t)depth * NSEG * CNT_PAD);
+            HIPCHK(hipMemcpy(cnt.data(), &g.d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+            for (int k = 1; k < depth; ++k) {
+                int64_t live = 0;
+                for (int q = 0; q < NSEG; ++q) live += cnt[((size_t)k * NSEG + q) * CNT_PAD];
+                if (live == 0) {
+                    depth = k;
+                    break;
+                }
+            }
+        }
+        *g.traced_depth = depth;
+    }
     return PT_OK;
 }
 

@@ -271,6 +271,7 @@ class PathTracer:
         _check(lib.pt_init(ctypes.byref(view), ctypes.byref(self.opts)), "pt_init")
         PathTracer._live = self
         self.iteration = 0
+        self._host_image = None
 
     @property
     def pixels(self):
@@ -279,9 +280,15 @@ class PathTracer:
     def trace(self, iteration: int | None = None, pbo_device_ptr: int | None = None, copy_image: bool = False):
         """One pathtrace(pbo, 0, iteration) call.  Returns the accumulated image if copy_image."""
         self.iteration = self.iteration + 1 if iteration is None else int(iteration)
-        img = np.empty((self.pixels, 3), np.float32) if copy_image else None
+        img = None
+        if copy_image:
+            # one host buffer per tracer, like the reference's scene->state.image: the library
+            # page-locks it on first use (the pointer must stay the same allocation)
+            if self._host_image is None:
+                self._host_image = np.empty((self.pixels, 3), np.float32)
+            img = self._host_image
         _check(lib.pt_trace(pbo_device_ptr, 0, self.iteration, _ptr(img)), "pt_trace")
-        return img
+        return None if img is None else img.copy()
 
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")
@@ -371,7 +378,8 @@ class PathTracer:
         return perm
 
     def free(self):
-        lib.pt_free()
+        lib.pt_free()               # also releases the page-locked host image
+        self._host_image = None
         if PathTracer._live is self:
             PathTracer._live = None
 

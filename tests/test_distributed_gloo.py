@@ -1,8 +1,8 @@
 """Multi-process (world_size 2, gloo, CPU) coverage of the multi-GPU frame logic in
 ptamd/dist.py: the PIXELS shard mapping, the SAMPLES iteration schedule and the framebuffer
 combine.  Each rank's per-pixel results come from the CPU oracle (pixels are independent, so
-which rank traces a pixel cannot change its value); the combine is the same
-torch.distributed.reduce the GPU path issues over RCCL."""
+which rank traces a pixel cannot change its value); the combine is the same TileGather /
+ImageReduce code bench.py runs over RCCL, here with gloo on host tensors."""
 import os
 import socket
 import sys
@@ -48,11 +48,23 @@ def test_sample_schedule_covers_each_iteration_once():
         assert its == list(range(1, 5 * world + 1))
 
 
-def _worker(rank, world, port, mode, out_dir):
+class _HostTracer:
+    """The slice of ptamd.PathTracer the combiners use, over an oracle-rendered host image."""
+
+    def __init__(self, img, w, h):
+        self.img, self.width, self.height = img, w, h
+
+    def image(self):
+        return self.img.copy()
+
+    def set_image(self, img):
+        self.img = np.asarray(img, np.float32).reshape(-1, 3).copy()
+
+
+def _worker(rank, world, port, mode, rows, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     sys.path.insert(0, PKG)
     sys.path.insert(0, ORACLE)
-    import torch
     import torch.distributed as dist
     import oracle as O
     from ptamd import dist as D
@@ -65,25 +77,26 @@ def _worker(rank, world, port, mode, out_dir):
             r.trace(it)
         img = r.image.copy()
         mask = np.zeros(h, bool)
-        mask[D.owned_rows(h, 8, world, rank)] = True
+        mask[D.owned_rows(h, rows, world, rank)] = True
         img[~np.repeat(mask, w)] = 0.0
+        tr = _HostTracer(img, w, h)
+        D.TileGather(tr, rows, world, rank, backend="gloo").run()    # the gather bench.py times
     else:
         for it in D.sample_iterations(-(-SPP // world), world, rank):
             if it <= SPP:
                 r.trace(it)
-        img = r.image.copy()
-    t = torch.from_numpy(img.reshape(-1).copy())
-    D.combine(t)
+        tr = _HostTracer(r.image.copy(), w, h)
+        D.ImageReduce(tr, rank, backend="gloo").run()
     if rank == 0:
-        np.save(os.path.join(out_dir, f"{mode}.npy"), t.numpy().reshape(-1, 3))
+        np.save(os.path.join(out_dir, f"{mode}.npy"), tr.image())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["pixels", "samples"])
-def test_two_rank_frame_combine(mode, tmp_path, oracle):
+@pytest.mark.parametrize("mode,world,rows", [("pixels", 2, 8), ("pixels", 3, 1), ("pixels", 2, 4), ("samples", 2, 8)])
+def test_multi_rank_frame_combine(mode, world, rows, tmp_path, oracle):
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(2, _free_port(), mode, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), mode, rows, str(tmp_path)), nprocs=world, join=True)
     got = np.load(tmp_path / f"{mode}.npy")
     sc = oracle.load_scene(scene_path("cornell"), res=RES)
     r = oracle.Renderer(sc, oracle.options(num_threads=1))
@@ -95,3 +108,22 @@ def test_two_rank_frame_combine(mode, tmp_path, oracle):
         fin = np.isfinite(r.image)
         np.testing.assert_allclose(got[fin], r.image[fin], rtol=2e-6, atol=1e-6)
         assert (np.isnan(got) == np.isnan(r.image)).all()
+
+
+def test_bench_shard_rows_split_evenly():
+    sys.path.insert(0, os.path.dirname(PKG))
+    import bench
+    for h, world in [(800, 1), (800, 2), (800, 8), (1600, 8), (800, 3), (20, 2)]:
+        rows = bench.shard_rows(h, world)
+        assert rows in (8, 4, 2, 1)
+        if h % world == 0:
+            assert h % (rows * world) == 0
+
+
+def test_bench_refuses_world_size_mismatch():
+    """--gpus must match the launcher's WORLD_SIZE (checked before any GPU work)"""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(PKG), "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr

@@ -10,11 +10,12 @@ tolerance of SURVEY §8c, checked in test_statistical_tolerance_vs_glibc_oracle.
 import json
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, PKG, scene_path
+from conftest import GOLDEN, PKG, REPO, scene_path
 
 pytestmark = pytest.mark.gpu
 
@@ -392,7 +393,7 @@ def test_statistical_tolerance_vs_glibc_oracle(oracle, ptamd):
     assert abs(g[fin].mean() - c[fin].mean()) / c[fin].mean() <= 1e-4
 
 
-def test_cpp_boundary_pt_render(tmp_path, oracle):
+def test_cpp_boundary_pt_render(tmp_path, oracle, ptamd):
     """The reference's C++ boundary (pathtraceInit / pathtrace / pathtraceFree) driven by the
     headless main.cpp replacement; its PFM (accumulated image) equals the oracle's."""
     exe = os.path.join(PKG, "build", "pt_render")
@@ -408,7 +409,11 @@ def test_cpp_boundary_pt_render(tmp_path, oracle):
     for it in (1, 2, 3):
         r.trace(it)
     assert _eq(data, r.image)
-    assert os.path.getsize(out + ".png") > 64 * 64 * 3
+    # the PNG is saveImage's (flip, 1/spp, clamp, x255) in stb_image_write's exact bytes
+    ref_png = str(tmp_path / "ref")
+    ptamd.save_png(r.image, 64, 64, 3, ref_png)
+    with open(out + ".png", "rb") as f, open(ref_png + ".png", "rb") as g:
+        assert f.read() == g.read()
 
 
 def test_pixel_shards_sum_to_full_frame(oracle, ptamd):
@@ -457,3 +462,136 @@ def test_intersections_match_reference(name, variant, ptamd):
     tr.free()
     assert int((got["t"] > 0).sum()) == ref["hits"]
     assert R.digest(R.pack(got, R.P_ISECT)) == ref["isect_sha256"]
+
+
+# ---- the configurations bench.py times, at their full size (round-1 VERDICT "What's weak" 2) ----
+@pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy"])
+def test_benched_configuration_bitexact(name, oracle, ptamd):
+    """Exactly what bench.py times for BASELINE configs[1] / configs[3]: 800x800, default options
+    (variant 186: block exchange, split BVH queue, pair layout), auto frames-per-pass (one 32-frame
+    wavefront pass), then a second partial pass.  Image and per-bounce live totals == the oracle's
+    (OpenMP over paths) frame by frame."""
+    a, b = _oracle_pair(oracle, ptamd, name, None)
+    tr = ptamd.PathTracer(b)
+    tr.trace_frames(1, 40)
+    st = tr.stats()
+    assert st["frames_per_pass"] == 32 and st["frames_total"] == 40
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tot = np.zeros(a.trace_depth, np.int64)
+    for it in range(1, 41):
+        tot += np.maximum(r.trace(it), 0)
+    assert st["live_total"][:a.trace_depth] == tot.tolist()
+    img = tr.image()
+    assert _eq(img, r.image), (name, int(np.sum(img.view(np.uint32) != r.image.view(np.uint32))))
+    tr.free()
+
+
+def test_config5_khaslana_1600_depth12(oracle, ptamd):
+    """BASELINE configs[4] at its stated size: cornell_obj_khaslana 1600x1600, depth 12 (stand-in
+    meshes, 49760 triangles), default options, 2 frames: image and live counts bit-exact."""
+    a, b = _oracle_pair(oracle, ptamd, "cornell_obj_khaslana", (1600, 1600), 12)
+    tr = ptamd.PathTracer(b)
+    tr.trace_frames(1, 2)
+    st = tr.stats()
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tot = np.zeros(12, np.int64)
+    for it in (1, 2):
+        tot += np.maximum(r.trace(it), 0)
+    assert st["live_total"][:12] == tot.tolist()
+    assert _eq(tr.image(), r.image)
+    tr.free()
+
+
+def test_api_frame_traced_depth_and_host_copy(oracle, ptamd):
+    """pathtrace() as main.cpp:463 calls it: F = 1, the accumulated image copied to the (page-
+    locked) host buffer every call, TracedDepth = the bounces the frame actually ran
+    (pathtrace.cu:759-770)."""
+    import ctypes
+    a, b = _oracle_pair(oracle, ptamd, "cornell", (64, 64))
+    td = ctypes.c_int32(-7)
+    ptamd.lib.pt_init_data_container(ctypes.byref(td))
+    tr = ptamd.PathTracer(b)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in (1, 2, 3):
+        live = r.trace(it)
+        img = tr.trace(it, copy_image=True)
+        assert _eq(img, r.image)
+        ran = next((k for k in range(1, a.trace_depth) if live[k] <= 0), a.trace_depth)
+        assert td.value == ran
+    tr.free()
+    # depth 1 scene: every path ends after one bounce
+    a1, b1 = _oracle_pair(oracle, ptamd, "cornell", (32, 32), 1)
+    tr = ptamd.PathTracer(b1)
+    tr.trace(1, copy_image=True)
+    assert td.value == 1
+    tr.free()
+    ptamd.lib.pt_init_data_container(None)
+
+
+def _skewed_mesh_scene(tmp_path, base, n=140000):
+    """cornell.json plus an OBJ of n small triangles whose x centroids shrink geometrically
+    (base^-(i mod 20000)): the reference's midpoint splits make a tree far deeper than its
+    reference-order DFS stack, with > 65535 node refs (no pair layout)."""
+    rng = np.random.default_rng(1)
+    k = np.arange(n) % 20000
+    c = np.stack([10.0 * base ** (-k.astype(np.float64)) - 5.0, 1.0 + 8.0 * rng.random(n),
+                  -4.0 + 8.0 * rng.random(n)], 1).astype(np.float32)
+    lines = []
+    for p in c:
+        lines.append("v %.6f %.6f %.6f\nv %.6f %.6f %.6f\nv %.6f %.6f %.6f" % (
+            p[0], p[1], p[2], p[0] + 0.02, p[1], p[2], p[0], p[1] + 0.02, p[2] + 0.01))
+    faces = "\n".join("f %d %d %d" % (3 * i + 1, 3 * i + 2, 3 * i + 3) for i in range(n))
+    (tmp_path / "mesh.obj").write_text("\n".join(lines) + "\n" + faces + "\n")
+    with open(scene_path("cornell")) as f:
+        d = json.load(f)
+    d["Objects"].append({"TYPE": "obj", "PATH": "/mesh.obj", "MATERIAL": "diffuse_red",
+                         "TRANS": [0, 0, 0], "ROTAT": [0, 0, 0], "SCALE": [1, 1, 1]})
+    path = tmp_path / "skewed.json"
+    path.write_text(json.dumps(d))
+    return str(path)
+
+
+@pytest.mark.parametrize("base", [1.001, 1.002])
+def test_deep_skewed_bvh_intersections(base, tmp_path, oracle, ptamd):
+    """Deep trees (height 43 / 71 against a reference DFS stack of 13 / 12, ~96k nodes): the
+    near-first traversal gets a stack of height + 1 (base 1.001), or, when that exceeds the 64
+    entries the reference's own stack holds, the reference-order traversal runs (base 1.002).
+    No push is dropped: full records bit-exact against the oracle on rays aimed at the triangles."""
+    import ctypes
+    import refpins as R
+    path = _skewed_mesh_scene(tmp_path, base)
+    a = oracle.load_scene(path, res=(96, 96))
+    b = ptamd.SceneFile(path, res=(96, 96))
+    assert len(a.bvh_nodes) > 65535
+    rays = R.rays(8192, seed=3, targets=R.scene_targets(b.geoms, b.triangles)).astype(ptamd.PATH)
+    tr = ptamd.PathTracer(b)
+    got = tr.test_intersect(rays)
+    tr.free()
+    want = np.zeros(len(rays), oracle.ISECT)
+    oracle.lib().or_compute_intersections(ctypes.byref(a.c_struct()), ctypes.byref(oracle.options()),
+                                          rays.ctypes.data, len(rays), want.ctypes.data)
+    assert (want["t"] > 0).sum() > 4000
+    assert R.digest(R.pack(got, R.P_ISECT)) == R.digest(R.pack(want, R.P_ISECT))
+
+
+def test_bench_two_ranks_pixel_tiles(tmp_path, oracle):
+    """`bench.py --gpus 2` (no launcher): the parent starts torch.distributed.run with 2 ranks
+    (gloo, sharing this GPU), each traces its interleaved row bands of 2 x (W + K) frames, rank 0
+    gathers the tiles; the line reports n_gpus 2 and the image is bit-identical to one GPU's."""
+    dump = tmp_path / "img.npy"
+    env = dict(os.environ, PT_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup",
+                        "1", "--no-cpu-baseline", "--no-configs", "--no-api", "--dump-image", str(dump)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["distributed"]["world_size"] == 2
+    assert line["scaling"] == "weak" and line["distributed"]["shard"] == "pixels"
+    a = oracle.load_scene(scene_path("cornell"))
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in range(1, 2 * (1 + 3) + 1):
+        r.trace(it)
+    got = np.load(dump)
+    assert _eq(got, r.image), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
