@@ -188,6 +188,16 @@ struct DevPair {
     float4 r_hi;   // right box max.xyz | right s
 };
 
+// VAR_BVH_QUAD: a 4-wide node collapsed from the reference's binary tree -- the up-to-4
+// grandchildren of an internal node (a child that is a leaf sits in its own slot).  Each child
+// box lies inside its parent's, and the reference's slab test is monotone in the box bounds, so
+// a grandchild that passes implies its parent passes: testing the grandchildren directly visits
+// exactly the leaves the binary traversal visits.  128 B = one cache line.
+struct DevQuad {
+    float4 lo[4];   // child box min.xyz | child ref (int bits; -1: empty slot)
+    float4 hi[4];   // child box max.xyz | child s (cull size)
+};
+
 // hot triangle record in leaf order (index k = node.start + i): 3 positions, 48 bytes
 struct DevTriHot {
     float4 a;   // v0.xyz, v1.x

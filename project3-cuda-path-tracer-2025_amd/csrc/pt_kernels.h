@@ -32,6 +32,8 @@ enum : int {
                            // queued and traversed (then shaded) by k_bvh_bounce in full waves
     VAR_BVH_NODES = 64,    // host only: BVH_FAST on the node array instead of the DevPair layout (A/B)
     VAR_BLOCK_REDIST = 128,  // with VAR_WAVE_REDIST: the exchange spans the block (block_intersect)
+    VAR_BVH_QUAD = 256,    // with VAR_BVH_FAST + pair layout: traverse 4-wide nodes (DevQuad) collapsed
+                           // from the binary tree (same leaves, same winner)
 };
 
 struct CamDev {
@@ -68,6 +70,8 @@ struct SceneDev {
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
+    const DevQuad* quads;     // VAR_BVH_QUAD layout (null: not built); leaves are refs >= num_quads
+    int num_quads, qroot_ref;
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
@@ -472,6 +476,113 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
     bv = st.bv;
     btri = st.btri;
     return st.t_hit;
+}
+
+// one step on the 4-wide layout: a quad expansion (4 exact box decisions + certified culls, the
+// nearest passing child continues, the others are pushed farthest first) or one leaf
+template <bool COUNT = false>
+PT_DEV void trav_step_quad(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
+    const int Q = sc.num_quads;
+    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
+    const int cur = st.cur;
+    bool next = false;
+    if (cur < Q) {
+        if (COUNT) n_nodes++;
+        const v4f* R = reinterpret_cast<const v4f*>(sc.quads + cur);
+        v4f lo[4], hi[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            lo[k] = R[k];
+            hi[k] = R[4 + k];
+        }
+        float e[4], T[4];
+        int r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r[k] = __float_as_int(lo[k][3]);
+            float ek = 0.f;
+            bool pk = r[k] >= 0 && aabb_decide(make_float4(lo[k][0], lo[k][1], lo[k][2], 0.f),
+                                               make_float4(hi[k][0], hi[k][1], hi[k][2], 0.f), st.ro, st.rd, st.rr,
+                                               st.exact, ek);
+            T[k] = pk ? cull_threshold(sc, ek, hi[k][3]) : 0.f;
+            pk = pk && !(t_best < T[k]);
+            e[k] = pk ? ek : __builtin_inff();
+            r[k] = pk ? r[k] : -1;
+        }
+        // nearest first: sort the 4 (entry, ref, T) by entry (5 compare-exchanges)
+        auto cx = [&](int a, int b) {
+            const bool sw = e[b] < e[a];
+            const float ea = e[a], ta = T[a];
+            const int ra = r[a];
+            e[a] = sw ? e[b] : ea; e[b] = sw ? ea : e[b];
+            T[a] = sw ? T[b] : ta; T[b] = sw ? ta : T[b];
+            r[a] = sw ? r[b] : ra; r[b] = sw ? ra : r[b];
+        };
+        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+        // refs of passing children in ascending entry order (NaN-free keys; -1 = none)
+        int first = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (first < 0 && r[k] >= 0) first = k;
+        if (first >= 0) {
+#pragma unroll
+            for (int k = 3; k >= 0; --k)
+                if (k != first && r[k] >= 0 && st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(r[k], T[k]);
+            st.cur = first == 0 ? r[0] : first == 1 ? r[1] : first == 2 ? r[2] : r[3];
+            next = true;
+        }
+    } else {
+        const int leaf = cur - Q, base = 4 * leaf;
+        if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
+        const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
+        v4f c[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) c[k] = L[k];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
+            const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
+            const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
+            float t, u, v;
+            if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
+                (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
+                st.t_hit = t;
+                st.bu = u;
+                st.bv = v;
+                st.btri = base + i;
+            }
+        }
+    }
+    if (!next) {
+        const float tb = __builtin_fminf(st.t_hit, st.t_limit);
+        st.cur = -1;
+        while (st.sp > 0) {
+            const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
+            if (!(tb < __uint_as_float(w << 16))) {
+                st.cur = (int)(w >> 16);
+                break;
+            }
+        }
+    }
+}
+
+template <bool COUNT = false>
+PT_DEV float bvh_intersect_quads(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
+                                 int& btri) {
+    int n_nodes = 0, n_tris = 0;
+    TravState st;
+    trav_begin(sc, st, ro, rd, t_limit);
+    if (st.cur >= 0) st.cur = sc.qroot_ref;
+    while (st.cur >= 0) {
+        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
+        trav_step_quad<COUNT>(sc, st, stack, n_nodes, n_tris);
+    }
+    if (COUNT) {
+        sec_add_lanes(SEC_N_NODES, n_nodes);
+        sec_add_lanes(SEC_N_TRIS, n_tris);
+        sec_add_lanes(SEC_N_BVH_RAYS, 1);
+    }
+    return trav_result(st, bu, bv, btri);
 }
 
 template <bool COUNT = false>

@@ -341,8 +341,9 @@ __global__ __launch_bounds__(BLOCK, 7) void k_bvh_bounce(SceneDev sc, QueueBuf q
         p.d = mk(b.x, b.y, b.z);
         float u = 0.f, v = 0.f;
         int tri = -1;
-        const float tb = bvh_intersect_pairs<(VAR & VAR_SECTION_TIMING) != 0>(sc, p.o, p.d, s_stack + tid, t_prim, u,
-                                                                             v, tri);
+        constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
+        const float tb = (VAR & VAR_BVH_QUAD) ? bvh_intersect_quads<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri)
+                                              : bvh_intersect_pairs<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
         const float4 c = q.C[gid], d = q.D[gid];
         p.pix = __float_as_int(q.A[gid].w);
         p.rb = __float_as_int(q.B[gid].w);
@@ -754,6 +755,7 @@ struct State {
     DevNode* d_nodes = nullptr;
     DevTriHot* d_hot = nullptr;
     DevPair* d_pairs = nullptr;
+    DevQuad* d_quads = nullptr;
     DevTriHot* d_hot4 = nullptr;
     float4* d_leaf9 = nullptr;
     DevTriCold* d_cold = nullptr;
@@ -869,6 +871,9 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 30: launch_bounce_t<FIRST, HAS_BVH, 30>(grid, in, out, b); break;   // redist + pair counters
         case 154: launch_bounce_t<FIRST, HAS_BVH, 154>(grid, in, out, b); break;
         case 186: launch_bounce_t<FIRST, HAS_BVH, 186>(grid, in, out, b); break;
+        case 190: launch_bounce_t<FIRST, HAS_BVH, 190>(grid, in, out, b); break;   // 186 + section counters
+        case 442: launch_bounce_t<FIRST, HAS_BVH, 442>(grid, in, out, b); break;   // 186 + 4-wide BVH
+        case 446: launch_bounce_t<FIRST, HAS_BVH, 446>(grid, in, out, b); break;   // 442 + section counters
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
     }
 }
@@ -877,6 +882,7 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
     if (!g.split) var &= ~VAR_BVH_SPLIT;
+    if (!g.sc.quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
     if (first) {
         if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
         else launch_bounce_v<true, false>(var, grid, in, out, b);
@@ -994,6 +1000,14 @@ int run_pass(int iter, int batch) {
 }
 int run_frame(int iter) { return run_pass(iter, 1); }
 
+// frames of the next pass when `remaining` frames are left: the passes of a run are balanced
+// (100 frames at F = 32 -> 4 x 25, not 32 + 32 + 32 + 4: a small last pass runs its launches
+// with a fraction of the paths in flight at nearly full per-launch cost)
+int pass_frames(int remaining) {
+    const int passes = (remaining + g.batch - 1) / g.batch;
+    return (remaining + passes - 1) / passes;
+}
+
 // max DFS stack the reference traversal can reach on this tree (no culling)
 int bvh_max_stack(const pt_bvh_node* nodes, int n) {
     if (n <= 0) return 0;
@@ -1038,7 +1052,7 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
 
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
+    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_quads, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
                     g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl,
                     g.queue.A, g.queue.B, g.queue.C, g.queue.D};
     for (void* p : ptrs)
@@ -1344,6 +1358,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0;
+    std::vector<DevQuad> quads;      // VAR_BVH_QUAD layout (empty: not built)
+    int quad_root_ref = 0, quad_count = 0;
     float4 pair_root_lo{}, pair_root_hi{};
     double cull_extent = 1.0;
     if (g.has_bvh) {
@@ -1574,6 +1590,65 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         }
                         for (int m = 0; m < 9; ++m) (&leaf9[9 * (size_t)k + m].x)[i] = comp9[m];
                     }
+                // VAR_BVH_QUAD: 4-wide nodes.  Heads are the root and every internal node two
+                // levels below a head; a head's slots are its grandchildren (a leaf child keeps
+                // its own slot).  Breadth-first numbering, leaves after the quads.
+                if (o.variant & VAR_BVH_QUAD) {
+                    std::vector<int> qid(nn, -1), heads, qlev;
+                    if (!is_leaf[0]) {
+                        qid[0] = 0;
+                        heads.push_back(0);
+                        qlev.push_back(1);
+                    }
+                    auto slots_of = [&](int h) {
+                        std::vector<int> sl;
+                        for (int x : {s->bvh_nodes[h].left, s->bvh_nodes[h].right}) {
+                            if (is_leaf[x]) {
+                                sl.push_back(x);
+                            } else {
+                                sl.push_back(s->bvh_nodes[x].left);
+                                sl.push_back(s->bvh_nodes[x].right);
+                            }
+                        }
+                        return sl;
+                    };
+                    int qh = heads.empty() ? 0 : 1;
+                    for (size_t i = 0; i < heads.size(); ++i)
+                        for (int c : slots_of(heads[i]))
+                            if (!is_leaf[c] && qid[c] < 0) {
+                                qid[c] = (int)heads.size();
+                                heads.push_back(c);
+                                qlev.push_back(qlev[i] + 1);
+                                qh = std::max(qh, qlev[i] + 1);
+                            }
+                    const int Q = (int)heads.size();
+                    // a quad level pushes at most 3 entries: the stack needs 3 qh + 1
+                    if ((int64_t)Q + L <= 65535 && 3 * qh + 1 <= MAXSTACK) {
+                        quads.assign(std::max(1, Q), DevQuad{});
+                        for (int i = 0; i < Q; ++i) {
+                            DevQuad& qd = quads[i];
+                            for (int k = 0; k < 4; ++k) {
+                                const int none = -1;
+                                float fnone;
+                                memcpy(&fnone, &none, 4);
+                                qd.lo[k] = make_float4(0.f, 0.f, 0.f, fnone);
+                                qd.hi[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                            }
+                            int k = 0;
+                            for (int c : slots_of(heads[i])) {
+                                const int rf = is_leaf[c] ? Q + id[c] : qid[c];
+                                float frf;
+                                memcpy(&frf, &rf, 4);
+                                qd.lo[k] = make_float4(nodes[c].lo.x, nodes[c].lo.y, nodes[c].lo.z, frf);
+                                qd.hi[k] = make_float4(nodes[c].hi.x, nodes[c].hi.y, nodes[c].hi.z, node_aux[c].y);
+                                ++k;
+                            }
+                        }
+                        quad_count = Q;
+                        quad_root_ref = is_leaf[0] ? id[0] : 0;
+                        g.stack_depth = std::max(g.stack_depth, 3 * qh + 1);
+                    }
+                }
                 pair_root_ref = ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
@@ -1611,6 +1686,10 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         RC(upload(g.d_nodes, nodes.data(), nodes.size()));
         RC(upload(g.d_hot, hot.data(), hot.size()));
         RC(upload(g.d_cold, cold.data(), cold.size()));
+        if (!quads.empty()) {
+            RC(dalloc(&g.d_quads, quads.size()));
+            RC(upload(g.d_quads, quads.data(), quads.size()));
+        }
         if (!pairs.empty()) {
             RC(dalloc(&g.d_pairs, pairs.size()));
             RC(upload(g.d_pairs, pairs.data(), pairs.size()));
@@ -1692,6 +1771,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.texinfo = g.d_texinfo;
     sc.num_textures = num_tex;
     sc.pairs = g.d_pairs;
+    sc.quads = g.d_quads;
+    sc.num_quads = quad_count;
+    sc.qroot_ref = quad_root_ref;
     sc.hot4 = g.d_hot4;
     sc.leaf9 = g.d_leaf9;
     sc.num_pairs = pair_count;
@@ -1771,7 +1853,7 @@ int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
     // passes of g.batch frames (bit-identical to frame-by-frame: k_combine keeps the order)
     for (int i = 0; i < count;) {
-        const int f = std::min(g.batch, count - i);
+        const int f = pass_frames(count - i);
         RC(run_pass(first_iteration + i, f));
         i += f;
     }
@@ -1782,10 +1864,12 @@ int32_t pt_prepare_frames(int32_t count) {
     RC(need_init());
     if (count < 0) return fail(PT_E_INVALID, "bad count");
     if (!g.opts.use_graph) return PT_OK;
-    // the pass sizes pt_trace_frames(., count) will replay: F, and the remainder
-    const int sizes[2] = {std::min(g.batch, count), count % g.batch};
-    for (int f : sizes)
-        if (f > 0 && !g.graph_exec[f]) RC(build_graph(f));
+    // the pass sizes pt_trace_frames(., count) will replay
+    for (int i = 0; i < count;) {
+        const int f = pass_frames(count - i);
+        if (!g.graph_exec[f]) RC(build_graph(f));
+        i += f;
+    }
     return PT_OK;
 }
 
@@ -2095,7 +2179,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     g_prof = &rec;
     int rc = PT_OK;
     for (int i = 0; i < count && rc == PT_OK;) {
-        const int f = std::min(g.batch, count - i);
+        const int f = pass_frames(count - i);
         pass_start.push_back(rec.size());
         rc = enqueue_pass(first_iteration + i, f);
         g.frames_done += f;

@@ -278,7 +278,9 @@ class PathTracer:
         return self.width * self.height
 
     def trace(self, iteration: int | None = None, pbo_device_ptr: int | None = None, copy_image: bool = False):
-        """One pathtrace(pbo, 0, iteration) call.  Returns the accumulated image if copy_image."""
+        """One pathtrace(pbo, 0, iteration) call.  With copy_image, returns the accumulated image
+        copied into this tracer's host buffer (the reference's scene->state.image): a view that
+        the next trace(copy_image=True) overwrites."""
         self.iteration = self.iteration + 1 if iteration is None else int(iteration)
         img = None
         if copy_image:
@@ -288,7 +290,7 @@ class PathTracer:
                 self._host_image = np.empty((self.pixels, 3), np.float32)
             img = self._host_image
         _check(lib.pt_trace(pbo_device_ptr, 0, self.iteration, _ptr(img)), "pt_trace")
-        return None if img is None else img.copy()
+        return img
 
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")

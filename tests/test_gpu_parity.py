@@ -515,7 +515,7 @@ def test_api_frame_traced_depth_and_host_copy(oracle, ptamd):
     for it in (1, 2, 3):
         live = r.trace(it)
         img = tr.trace(it, copy_image=True)
-        assert _eq(img, r.image)
+        assert _eq(img, r.image) and img is tr.trace.__self__._host_image
         ran = next((k for k in range(1, a.trace_depth) if live[k] <= 0), a.trace_depth)
         assert td.value == ran
     tr.free()
