@@ -160,6 +160,11 @@ typedef struct pt_scene_file pt_scene_file;
  * main.cpp:359-380 + 423-444, the camera the reference's frames are rendered with. */
 int32_t pt_scene_load(const char* json_path, int32_t res_x, int32_t res_y, int32_t depth, int32_t viewer_camera,
                       pt_scene_file** out);
+/* Same, with flags: PT_SCENE_VIEWER_CAMERA (= viewer_camera above), PT_SCENE_GPU_BVH (build the BVH
+ * on the current HIP device with pt_bvh_build instead of on the host; the same nodes and triIndices). */
+enum { PT_SCENE_VIEWER_CAMERA = 1, PT_SCENE_GPU_BVH = 2 };
+int32_t pt_scene_load_ex(const char* json_path, int32_t res_x, int32_t res_y, int32_t depth, int32_t flags,
+                         pt_scene_file** out);
 /* View borrowed from the scene file (valid until pt_scene_free). */
 int32_t pt_scene_get_view(const pt_scene_file* scene, pt_scene_view* view);
 int32_t pt_scene_get_info(const pt_scene_file* scene, int32_t* iterations, int32_t* trace_depth, char* image_name,
@@ -171,6 +176,15 @@ const char* pt_scene_last_error(void);
  * Writes width/height; copies w*h*4 bytes into rgba when cap is large enough (rgba may be
  * NULL to query the size).  PT_E_INVALID + pt_scene_last_error() on a decode failure. */
 int32_t pt_texture_load(const char* path, int32_t* width, int32_t* height, uint8_t* rgba, int64_t cap);
+
+/* Scene::buildBVH + buildBVHRecursive (scene.cpp:445-525) on the current HIP device: bounds,
+ * longest-axis midpoint split, the in-place swap partition and the median fallback, level by level
+ * on the GPU, with the reference's preorder node numbering -- the same bvhNodes and triIndices as the
+ * host build, bit for bit (csrc/pt_bvh_build.hip).  `nodes` holds cap >= 2n - 1 entries;
+ * *num_nodes receives the count; tri_indices receives n entries.  PT_E_NODEVICE without a GPU. */
+int32_t pt_bvh_build(const pt_triangle* triangles, int32_t n, pt_bvh_node* nodes, int32_t cap, int32_t* num_nodes,
+                     int32_t* tri_indices);
+const char* pt_bvh_build_last_error(void);
 
 /* saveImage (main.cpp:395-419) + Image::savePNG (image.cpp:23-43): writes "<base_path>.png" from an
  * accumulated host image (width*height*3 floats) traced `iteration` samples per pixel — x-flipped,

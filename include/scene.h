@@ -43,8 +43,9 @@ class Scene {
 public:
     // scene.cpp:22-37; throws std::runtime_error where the reference exit()s / throws
     explicit Scene(std::string filename);
-    // same, with RES (<= 0: keep) / DEPTH (< 0: keep) overridden before the camera is derived
-    Scene(std::string filename, int resx, int resy, int depth);
+    // same, with RES (<= 0: keep) / DEPTH (< 0: keep) overridden before the camera is derived;
+    // gpuBVH: build the BVH with pt_bvh_build on the current HIP device (same tree, bit for bit)
+    Scene(std::string filename, int resx, int resy, int depth, bool gpuBVH = false);
     ~Scene();
 
     std::vector<Geom> geoms;
@@ -66,6 +67,7 @@ private:
     void loadFromOBJ(const std::string& objName, int materialID, const pt_mat4& transformMatrix,
                      const pt_mat4& invTransposeMatrix);
     void buildBVH();
+    bool gpuBVH = false;
     int loadTexture(const std::string& texturePath);
 };
 

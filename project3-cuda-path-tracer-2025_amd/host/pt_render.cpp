@@ -5,7 +5,7 @@
 // accumulated float image as PFM.
 //
 //   pt_render SCENE.json [--spp N] [--res WxH] [--depth D] [--out PREFIX]
-//             [--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K]
+//             [--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K] [--gpu-bvh]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,10 +18,11 @@
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::printf("Usage: %s SCENEFILE.json [--spp N] [--res WxH] [--depth D] [--out PREFIX] "
-                    "[--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K]\n", argv[0]);
+                    "[--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K] [--gpu-bvh]\n", argv[0]);
         return 1;
     }
     std::string scene_file = argv[1], out;
+    bool gpu_bvh = false;
     int spp = -1, resx = 0, resy = 0, depth = -1;
     pt_options opts;
     pt_default_options(&opts);
@@ -40,11 +41,12 @@ int main(int argc, char** argv) {
         else if (a == "--no-compaction") opts.stream_compaction = 0;
         else if (a == "--no-bvh") opts.bvh = 0;
         else if (a == "--device") opts.device = std::atoi(next());
+        else if (a == "--gpu-bvh") gpu_bvh = true;
         else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
     Scene* scene = nullptr;
     try {
-        scene = new Scene(scene_file, resx, resy, depth);
+        scene = new Scene(scene_file, resx, resy, depth, gpu_bvh);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

@@ -349,7 +349,7 @@ void applyViewerCamera(Camera& cam) {
 
 Scene::Scene(std::string filename) : Scene(std::move(filename), 0, 0, -1) {}
 
-Scene::Scene(std::string filename, int resx, int resy, int depth) {
+Scene::Scene(std::string filename, int resx, int resy, int depth, bool gpu_bvh) : gpuBVH(gpu_bvh) {
     auto dot_pos = filename.find_last_of('.');
     std::string ext = dot_pos == std::string::npos ? "" : filename.substr(dot_pos);
     if (ext != ".json") throw std::runtime_error("Couldn't read from " + filename);   // scene.cpp:30-35
@@ -541,6 +541,16 @@ void Scene::buildBVH() {
     triIndices.resize(triangles.size());
     for (int i = 0; i < (int)triangles.size(); i++) triIndices[i] = i;
     if (triangles.empty()) return;
+    if (gpuBVH) {   // the same recursion on the GPU (csrc/pt_bvh_build.hip), same bits
+        const int n = (int)triangles.size();
+        bvhNodes.resize(2 * (size_t)n - 1);
+        int32_t count = 0;
+        const int32_t rc = pt_bvh_build(triangles.data(), n, bvhNodes.data(), (int32_t)bvhNodes.size(), &count,
+                                        triIndices.data());
+        if (rc != PT_OK) throw std::runtime_error(std::string("GPU BVH build: ") + pt_bvh_build_last_error());
+        bvhNodes.resize((size_t)count);
+        return;
+    }
     bvhNodes.reserve(2 * triangles.size());
     BVHBuilder b{triangles, bvhNodes, triIndices};
     b.build(0, (int)triangles.size());

@@ -39,10 +39,15 @@ int32_t pt_texture_load(const char* path, int32_t* width, int32_t* height, uint8
 // recompute (what every reference frame actually renders with)
 int32_t pt_scene_load(const char* path, int32_t resx, int32_t resy, int32_t depth, int32_t viewer_camera,
                       pt_scene_file** out) {
+    return pt_scene_load_ex(path, resx, resy, depth, viewer_camera ? PT_SCENE_VIEWER_CAMERA : 0, out);
+}
+
+int32_t pt_scene_load_ex(const char* path, int32_t resx, int32_t resy, int32_t depth, int32_t flags,
+                         pt_scene_file** out) {
     if (!path || !out) return PT_E_INVALID;
     try {
-        Scene* s = new Scene(path, resx, resy, depth);
-        if (viewer_camera) applyViewerCamera(s->state.camera);
+        Scene* s = new Scene(path, resx, resy, depth, (flags & PT_SCENE_GPU_BVH) != 0);
+        if (flags & PT_SCENE_VIEWER_CAMERA) applyViewerCamera(s->state.camera);
         *out = new pt_scene_file{s};
         return PT_OK;
     } catch (const std::exception& e) {

@@ -91,7 +91,7 @@ ABI_SYMBOLS = [
     "pt_get_frame_stats", "pt_reset_stats", "pt_set_camera", "pt_scene_load", "pt_scene_get_view", "pt_scene_get_info",
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
-    "pt_save_png", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
+    "pt_save_png", "pt_scene_load_ex", "pt_bvh_build", "pt_bvh_build_last_error", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
 ]
 
 
@@ -119,6 +119,9 @@ def _load():
         "pt_debug_section_counters": (i32, [vp, i32, i32]),
         "pt_texture_load": (i32, [ctypes.c_char_p, vp, vp, vp, i64]),
         "pt_save_png": (i32, [vp, i32, i32, i32, ctypes.c_char_p]),
+        "pt_scene_load_ex": (i32, [ctypes.c_char_p, i32, i32, i32, i32, vp]),
+        "pt_bvh_build": (i32, [vp, i32, vp, i32, vp, vp]),
+        "pt_bvh_build_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -169,11 +172,12 @@ class _TextureC(ctypes.Structure):
 class SceneFile:
     """The reference's Scene (scene.h:6-28) loaded by the framework's C++ loader."""
 
-    def __init__(self, path: str, res=None, depth=None, viewer_camera: bool = True):
+    def __init__(self, path: str, res=None, depth=None, viewer_camera: bool = True, gpu_bvh: bool = False):
         h = ctypes.c_void_p()
         rx, ry = (res if res is not None else (0, 0))
-        rc = lib.pt_scene_load(path.encode(), int(rx), int(ry), -1 if depth is None else int(depth), int(bool(viewer_camera)),
-                               ctypes.byref(h))
+        flags = (1 if viewer_camera else 0) | (2 if gpu_bvh else 0)
+        rc = lib.pt_scene_load_ex(path.encode(), int(rx), int(ry), -1 if depth is None else int(depth), flags,
+                                  ctypes.byref(h))
         if rc != PT_OK:
             raise PtError(f"pt_scene_load({path}): {lib.pt_scene_last_error().decode(errors='replace')}")
         self._h = h
@@ -392,6 +396,20 @@ def rng_draws(seeds: np.ndarray, n: int) -> np.ndarray:
     out = np.zeros((len(seeds), n), np.float32)
     _check(lib.pt_test_rng(_ptr(seeds), len(seeds), int(n), _ptr(out)), "pt_test_rng")
     return out
+
+
+def build_bvh(triangles: np.ndarray):
+    """scene.cpp:445-525 on the GPU (pt_bvh_build): (bvh_nodes, tri_indices), bit-identical to the
+    host build."""
+    tris = np.ascontiguousarray(triangles, TRIANGLE)
+    n = len(tris)
+    nodes = np.zeros(max(1, 2 * n - 1), BVHNODE)
+    idx = np.zeros(max(1, n), np.int32)
+    cnt = ctypes.c_int32()
+    rc = lib.pt_bvh_build(_ptr(tris), n, nodes.ctypes.data, len(nodes), ctypes.byref(cnt), idx.ctypes.data)
+    if rc != PT_OK:
+        raise PtError(f"pt_bvh_build: {lib.pt_bvh_build_last_error().decode(errors='replace')} (code {rc})")
+    return nodes[:cnt.value].copy(), idx[:n].copy()
 
 
 def save_png(image: np.ndarray, width: int, height: int, iteration: int, base_path: str):

@@ -595,3 +595,68 @@ def test_bench_two_ranks_pixel_tiles(tmp_path, oracle):
         r.trace(it)
     got = np.load(dump)
     assert _eq(got, r.image), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
+
+
+# ---- GPU BVH build (csrc/pt_bvh_build.hip) == scene.cpp:445-525, bit for bit ----
+def _oracle_bvh(oracle, tris):
+    n = len(tris)
+    nodes = np.zeros(max(1, 2 * n), oracle.BVHNODE)
+    idx = np.zeros(max(1, n), np.int32)
+    nn = oracle.lib().or_build_bvh(tris.ctypes.data, n, nodes.ctypes.data, idx.ctypes.data) if n else 0
+    return nodes[:nn], idx[:n]
+
+
+def _adversarial_tris(oracle, kind, n, seed):
+    """triangles whose build exercises ties, signed zeros, NaN coordinates, equal centroids
+    (median fallback) and long swap-partition chains"""
+    rng = np.random.default_rng(seed)
+    t = np.zeros(n, oracle.TRIANGLE)
+    if kind == "random":
+        p = rng.standard_normal((n, 3, 3)).astype(np.float32)
+    elif kind == "grid":          # many equal coordinates and centroids, +-0
+        p = (rng.integers(-2, 3, (n, 3, 3)) * 0.5).astype(np.float32)
+        p[rng.random((n, 3, 3)) < 0.2] = -0.0
+    elif kind == "same":          # identical centroids: every split falls back to the median
+        p = np.tile(np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32), (n, 1, 1))
+    elif kind == "nan":           # NaN coordinates (the glm min/max fold resets on them)
+        p = rng.standard_normal((n, 3, 3)).astype(np.float32)
+        p[rng.random((n, 3, 3)) < 0.05] = np.nan
+    else:                         # "alternating": less / not-less alternate along the range
+        x = np.where(np.arange(n) % 2 == 0, -1.0, 1.0) * (1 + np.arange(n) / n)
+        p = np.zeros((n, 3, 3), np.float32)
+        p[:, :, 0] = x[:, None]
+        p[:, 1, 1] = 0.01
+        p[:, 2, 2] = 0.01
+    for k, v in enumerate(("v1", "v2", "v3")):
+        t[v]["position"] = p[:, k]
+    t["centroid"] = ((p[:, 0] + p[:, 1] + p[:, 2]) / np.float32(3)).astype(np.float32)
+    return t
+
+
+@pytest.mark.parametrize("kind,n", [("random", 1), ("random", 4), ("random", 5), ("random", 37), ("random", 20000),
+                                    ("grid", 3000), ("same", 1000), ("nan", 2000), ("alternating", 4097)])
+def test_gpu_bvh_build_bitexact(kind, n, oracle, ptamd):
+    tris = _adversarial_tris(oracle, kind, n, n)
+    want_nodes, want_idx = _oracle_bvh(oracle, tris)
+    nodes, idx = ptamd.build_bvh(tris)
+    assert len(nodes) == len(want_nodes)
+    assert nodes.tobytes() == want_nodes.tobytes()
+    assert idx.tobytes() == want_idx.tobytes()
+
+
+@pytest.mark.parametrize("name", ["cornell_obj_bnnuy", "cornell_obj_khaslana", "cornell_obj_phatphuck"])
+def test_scene_gpu_bvh_matches_host_and_reference(name, ptamd):
+    """SceneFile(gpu_bvh=True) builds the tree on the GPU: the same nodes / triIndices as the
+    host build, hence the reference's (tests/golden/ref_pin.json digests)."""
+    import refpins as R
+    ref = _REF_PIN["scenes"][name]["sha256"]
+    g = ptamd.SceneFile(scene_path(name), viewer_camera=False, gpu_bvh=True)
+    assert R.digest(R.pack(g.bvh_nodes, R.P_BVHNODE)) == ref["bvhNodes"]
+    assert R.digest(g.tri_indices.astype("<i4")) == ref["triIndices"]
+
+
+def test_deep_skewed_gpu_bvh(tmp_path, oracle, ptamd):
+    path = _skewed_mesh_scene(tmp_path, 1.002, n=60000)
+    h = ptamd.SceneFile(path, viewer_camera=False)
+    g = ptamd.SceneFile(path, viewer_camera=False, gpu_bvh=True)
+    assert g.bvh_nodes.tobytes() == h.bvh_nodes.tobytes() and g.tri_indices.tobytes() == h.tri_indices.tobytes()
