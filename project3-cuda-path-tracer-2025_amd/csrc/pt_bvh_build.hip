@@ -12,7 +12,8 @@
 //   partition: the in-place swap loop `if (c < split) swap(idx[i], idx[mid++])` (Lomuto)
 //   median fallback when one side is empty; children: left (preorder next), then right
 //
-// GPU formulation, level by level (all nodes of one depth at once, one workgroup per node):
+// GPU formulation, level by level (all nodes of one depth at once; a node's range is cut into
+// pieces of 4096 triangles, one workgroup per piece, so the top levels fill the chip too):
 //   * bounds: each thread folds a contiguous chunk in order into a summary (value, "holds a
 //     NaN"), and chunks are joined pairwise in order (stride doubling).  The join is
 //     associative, so the result equals the sequential fold, signed zeros and NaNs included;
@@ -20,7 +21,7 @@
 //     start + k.  A "not less" element is moved only by a swap: the one at position p (which
 //     is mid at that moment) jumps to the index of the (p - start)-th less element.  So its final
 //     slot is the fixed point of J(p) = lessIdx[p - start] for p < start + nLess, J(p) = p
-//     beyond -- resolved by pointer jumping.  (Checked against the loop itself on 20k random
+//     beyond -- resolved by grid-wide pointer jumping (ceil(log2 len) + 1 rounds).  (Checked against the loop itself on 20k random
 //     sequences while deriving it; the GPU result is checked against host/scene.cpp's
 //     sequential builder in tests/test_gpu_parity.py::test_gpu_bvh_build_bitexact.)
 //   * node numbering is the reference's preorder; it needs the subtree sizes, so the host keeps
@@ -28,8 +29,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <chrono>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -39,12 +43,6 @@
 namespace {
 
 constexpr int BT = 256;   // threads per workgroup
-
-struct Seg {
-    int start, end;       // triangle range
-    int axis;             // split axis (build kernel output)
-    float split;          // split position
-};
 
 // glm 0.9.6 (func_common.inl:409-435): min(x, y) = x < y ? x : y, max(x, y) = x > y ? x : y.
 // Folded as acc = min(acc, v): ties go to the LATER element (the sign of a zero bound), and a
@@ -89,23 +87,35 @@ __device__ __forceinline__ const float* tri_f(const pt_triangle* t, int i) {
 constexpr int OFF_V[3] = {1, 10, 19};
 constexpr int OFF_C = 27;
 
-// node bounds + centroid bounds of one segment; out[12 * s]: min.xyz max.xyz cmin.xyz cmax.xyz
-__global__ __launch_bounds__(BT) void k_seg_bounds(const pt_triangle* __restrict__ tris, const int* __restrict__ idx,
-                                                   const Seg* __restrict__ segs, float* __restrict__ out) {
+// ---- level kernels.  A node's triangle range is cut into pieces of up to PIECE elements, so a
+// large node (the top levels) is spread over many workgroups. ----
+constexpr int PIECE = 4096;
+
+struct Piece {
+    int seg;              // index of the node (segment) in this level's list
+    int start, end;       // element range of the piece
+};
+
+__device__ __forceinline__ bool is_min_comp(int k) { return k < 3 || (k >= 6 && k < 9); }
+
+// fold of one piece (12 components: node min.xyz max.xyz, centroid min.xyz max.xyz), threads fold
+// contiguous sub-ranges in order, then join in order
+__global__ __launch_bounds__(BT) void k_piece_fold(const pt_triangle* __restrict__ tris, const int* __restrict__ idx,
+                                                   const Piece* __restrict__ pieces, float* __restrict__ pv,
+                                                   int* __restrict__ pf) {
     __shared__ float rv[12][BT];
     __shared__ int rf[12][BT];
-    const Seg sg = segs[blockIdx.x];
-    const int len = sg.end - sg.start;
+    const Piece pc = pieces[blockIdx.x];
+    const int len = pc.end - pc.start;
     const int chunk = (len + BT - 1) / BT;
-    const int a = sg.start + threadIdx.x * chunk;
-    const int b = min(sg.end, a + chunk);
+    const int a = pc.start + threadIdx.x * chunk;
+    const int b = min(pc.end, a + chunk);
     Fold f[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) f[k] = Fold{0.f, 1};
     for (int i = a; i < b; ++i) {
         const float* t = tri_f(tris, idx[i]);
-        // UpdateNodeBounds order: min over v1, v2, v3 then max over v1, v2, v3 (per component
-        // these are independent folds, each in element order)
+        // UpdateNodeBounds: per component, min / max over v1, v2, v3 of each triangle in order
 #pragma unroll
         for (int q = 0; q < 3; ++q)
 #pragma unroll
@@ -125,15 +135,14 @@ __global__ __launch_bounds__(BT) void k_seg_bounds(const pt_triangle* __restrict
         rf[k][threadIdx.x] = f[k].flags;
     }
     __syncthreads();
-    // in-order pairwise join: slot i covers chunks [i, i + 2s) after the step of stride s
+    // in-order pairwise join: slot i covers sub-ranges [i, i + 2s) after the step of stride s
     for (int s = 1; s < BT; s <<= 1) {
         const int i = threadIdx.x;
         if ((i & (2 * s - 1)) == 0) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) {
                 const Fold x{rv[k][i], rf[k][i]}, y{rv[k][i + s], rf[k][i + s]};
-                const bool mn = (k < 3) || (k >= 6 && k < 9);
-                const Fold z = mn ? fold_join<true>(x, y) : fold_join<false>(x, y);
+                const Fold z = is_min_comp(k) ? fold_join<true>(x, y) : fold_join<false>(x, y);
                 rv[k][i] = z.val;
                 rf[k][i] = z.flags;
             }
@@ -141,83 +150,182 @@ __global__ __launch_bounds__(BT) void k_seg_bounds(const pt_triangle* __restrict
         __syncthreads();
     }
     if (threadIdx.x < 12) {
-        const int k = threadIdx.x;
-        const Fold z{rv[k][0], rf[k][0]};
-        const bool mn = (k < 3) || (k >= 6 && k < 9);
-        out[12 * blockIdx.x + k] = mn ? fold_final<true>(z) : fold_final<false>(z);
+        pv[12 * blockIdx.x + threadIdx.x] = rv[threadIdx.x][0];
+        pf[12 * blockIdx.x + threadIdx.x] = rf[threadIdx.x][0];
     }
 }
 
-// the swap-partition of one segment (closed form, see the header): idx_in -> idx_out on
-// [start, end); nless[s] = number of "less" elements.  J / Jn: pointer-jumping scratch.
-__global__ __launch_bounds__(BT) void k_seg_partition(const pt_triangle* __restrict__ tris, const int* __restrict__ idx_in,
-                                                      int* __restrict__ idx_out, const Seg* __restrict__ segs,
-                                                      int* __restrict__ J, int* __restrict__ Jn, int* __restrict__ nless) {
-    __shared__ int scan[BT];
-    __shared__ int changed;
-    const Seg sg = segs[blockIdx.x];
-    const int len = sg.end - sg.start;
-    const int chunk = (len + BT - 1) / BT;
-    const int a = sg.start + threadIdx.x * chunk;
-    const int b = min(sg.end, a + chunk);
-    auto less = [&](int p) { return tri_f(tris, idx_in[p])[OFF_C + sg.axis] < sg.split; };
-    int cnt = 0;
-    for (int i = a; i < b; ++i) cnt += less(i) ? 1 : 0;
-    scan[threadIdx.x] = cnt;
+// join the pieces of each node in order and apply the fold's FLT_MAX / -FLT_MAX start
+__global__ void k_seg_fold(const int* __restrict__ first_piece, const float* __restrict__ pv,
+                           const int* __restrict__ pf, float* __restrict__ out, int nseg) {
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 4), k = threadIdx.x & 15;
+    if (s >= nseg || k >= 12) return;
+    Fold z{0.f, 1};
+    for (int p = first_piece[s]; p < first_piece[s + 1]; ++p) {
+        const Fold y{pv[12 * p + k], pf[12 * p + k]};
+        z = is_min_comp(k) ? fold_join<true>(z, y) : fold_join<false>(z, y);
+    }
+    out[12 * s + k] = is_min_comp(k) ? fold_final<true>(z) : fold_final<false>(z);
+}
+
+struct Split {
+    int axis;
+    float split;
+};
+
+// the swap partition, step 1: per piece of a split node, flag the "less" elements and count them
+__global__ __launch_bounds__(BT) void k_piece_count(const pt_triangle* __restrict__ tris, const int* __restrict__ idx,
+                                                    const Piece* __restrict__ pieces, const Split* __restrict__ splits,
+                                                    unsigned char* __restrict__ less, int* __restrict__ cnt) {
+    __shared__ int red[BT];
+    const Piece pc = pieces[blockIdx.x];
+    const Split sp = splits[pc.seg];
+    int c = 0;
+    for (int p = pc.start + (int)threadIdx.x; p < pc.end; p += BT) {
+        const bool l = tri_f(tris, idx[p])[OFF_C + sp.axis] < sp.split;
+        less[p] = l ? 1 : 0;
+        c += l ? 1 : 0;
+    }
+    red[threadIdx.x] = c;
     __syncthreads();
-    for (int s = 1; s < BT; s <<= 1) {   // inclusive scan (Hillis-Steele)
-        const int x = threadIdx.x >= s ? scan[threadIdx.x - s] : 0;
+    for (int s = BT / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cnt[blockIdx.x] = red[0];
+}
+
+// step 2: per split node, the exclusive scan of its pieces' counts (pieces of a node are
+// consecutive) and the node's "less" total
+__global__ void k_seg_scan(const int* __restrict__ first_piece, int* __restrict__ cnt_to_off, int* __restrict__ nless,
+                           int nseg) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    int run = 0;
+    for (int p = first_piece[s]; p < first_piece[s + 1]; ++p) {
+        const int c = cnt_to_off[p];
+        cnt_to_off[p] = run;
+        run += c;
+    }
+    nless[s] = run;
+}
+
+// step 3: the k-th "less" element of the node lands at start + k; J[start + k] = its position
+// (the slot the "not less" element sitting at start + k is swapped out to)
+__global__ __launch_bounds__(BT) void k_piece_place(const int* __restrict__ idx_in, int* __restrict__ idx_out,
+                                                    const Piece* __restrict__ pieces, const int* __restrict__ seg_start,
+                                                    const unsigned char* __restrict__ less, const int* __restrict__ off,
+                                                    int* __restrict__ J) {
+    __shared__ int scan[BT];
+    const Piece pc = pieces[blockIdx.x];
+    const int len = pc.end - pc.start;
+    const int chunk = (len + BT - 1) / BT;
+    const int a = pc.start + threadIdx.x * chunk;
+    const int b = min(pc.end, a + chunk);
+    int c = 0;
+    for (int i = a; i < b; ++i) c += less[i];
+    scan[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = 1; s < BT; s <<= 1) {   // inclusive Hillis-Steele scan
+        const int x = (int)threadIdx.x >= s ? scan[threadIdx.x - s] : 0;
         __syncthreads();
         scan[threadIdx.x] += x;
         __syncthreads();
     }
-    const int total = scan[BT - 1];
-    int r = scan[threadIdx.x] - cnt;   // rank of this chunk's first "less" element
-    // the k-th less element lands at start + k; J[start + k] = its position (the hop target of
-    // the element the swap at that moment moves out of slot start + k)
-    for (int i = a; i < b; ++i) {
-        if (less(i)) {
-            idx_out[sg.start + r] = idx_in[i];
-            J[sg.start + r] = i;
+    int r = seg_start[pc.seg] + off[blockIdx.x] + scan[threadIdx.x] - c;
+    for (int i = a; i < b; ++i)
+        if (less[i]) {
+            idx_out[r] = idx_in[i];
+            J[r] = i;
             ++r;
         }
-    }
-    __syncthreads();
-    const int lim = sg.start + total;
-    for (int p = sg.start + (int)threadIdx.x; p < sg.end; p += BT)
-        if (p >= lim) J[p] = p;
-    __threadfence_block();
-    __syncthreads();
-    // pointer jumping to the fixed point: every chain ends in a slot >= start + total
-    int* cur = J;
-    int* nxt = Jn;
-    for (;;) {
-        if (threadIdx.x == 0) changed = 0;
-        __syncthreads();
-        for (int p = sg.start + (int)threadIdx.x; p < sg.end; p += BT) {
-            const int j = cur[p];
-            const int jj = cur[j];
-            nxt[p] = jj;
-            if (jj != j) changed = 1;
-        }
-        __threadfence_block();
-        __syncthreads();
-        int* t = cur;
-        cur = nxt;
-        nxt = t;
-        if (!changed) break;
-        __syncthreads();
-    }
-    for (int i = a; i < b; ++i)
-        if (!less(i)) idx_out[cur[i]] = idx_in[i];
-    if (threadIdx.x == 0) nless[blockIdx.x] = total;
 }
 
-// leaf segments keep their order
-__global__ __launch_bounds__(BT) void k_seg_copy(const int* __restrict__ idx_in, int* __restrict__ idx_out,
-                                                 const Seg* __restrict__ segs) {
-    const Seg sg = segs[blockIdx.x];
-    for (int p = sg.start + (int)threadIdx.x; p < sg.end; p += BT) idx_out[p] = idx_in[p];
+// ---- small nodes (<= SMALL triangles: the bulk of the lower levels): one thread each, the
+// reference's sequential loops verbatim ----
+constexpr int SMALL = 256;
+
+struct SmallSeg {
+    int slot;             // index of the node in this level's list (bounds slot)
+    int start, end;
+};
+
+__global__ void k_small_bounds(const pt_triangle* __restrict__ tris, const int* __restrict__ idx,
+                               const SmallSeg* __restrict__ segs, float* __restrict__ out, int nseg) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const SmallSeg sg = segs[s];
+    float v[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        v[k] = FLT_MAX;
+        v[3 + k] = -FLT_MAX;
+        v[6 + k] = FLT_MAX;
+        v[9 + k] = -FLT_MAX;
+    }
+    for (int i = sg.start; i < sg.end; ++i) {   // UpdateNodeBounds (scene.cpp:429-442), then the centroid loop
+        const float* t = tri_f(tris, idx[i]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                v[k] = glm_min(v[k], t[OFF_V[q] + k]);
+                v[3 + k] = glm_max(v[3 + k], t[OFF_V[q] + k]);
+            }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[6 + k] = glm_min(v[6 + k], t[OFF_C + k]);
+            v[9 + k] = glm_max(v[9 + k], t[OFF_C + k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) out[12 * sg.slot + k] = v[k];
+}
+
+// the swap loop itself (scene.cpp:503-511) on one small split node; its elements are marked done
+// (less = 2) so the grid-wide scatter leaves them alone
+__global__ void k_small_partition(const pt_triangle* __restrict__ tris, const int* __restrict__ idx_in,
+                                  int* __restrict__ idx_out, const SmallSeg* __restrict__ segs,
+                                  const Split* __restrict__ splits, unsigned char* __restrict__ less,
+                                  int* __restrict__ nless, int nseg) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nseg) return;
+    const SmallSeg sg = segs[s];
+    const Split sp = splits[s];
+    for (int i = sg.start; i < sg.end; ++i) {
+        idx_out[i] = idx_in[i];
+        less[i] = 2;
+    }
+    int mid = sg.start;
+    for (int i = sg.start; i < sg.end; ++i) {
+        const int ti = idx_out[i];
+        if (tri_f(tris, ti)[OFF_C + sp.axis] < sp.split) {
+            idx_out[i] = idx_out[mid];
+            idx_out[mid] = ti;
+            mid++;
+        }
+    }
+    nless[s] = mid - sg.start;
+}
+
+__global__ void k_fill(int* __restrict__ J, unsigned char* __restrict__ less, int n) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) {
+        J[p] = p;
+        less[p] = 0;
+    }
+}
+// the chain J(p) = position of the (p - start)-th less element, for p < start + nless; J(p) = p
+// beyond.  Positions rise along a chain, so ceil(log2 len) + 1 jumping rounds reach the ends.
+__global__ void k_jump(const int* __restrict__ J, int* __restrict__ Jn, int n) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) Jn[p] = J[J[p]];
+}
+// every "not less" element (and every element of a leaf) goes to the end of its chain
+__global__ void k_scatter_rest(const int* __restrict__ idx_in, int* __restrict__ idx_out, const int* __restrict__ J,
+                               const unsigned char* __restrict__ less, int n) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n && !less[p]) idx_out[J[p]] = idx_in[p];
 }
 
 std::string g_err;
@@ -248,14 +356,25 @@ extern "C" int32_t pt_bvh_build(const pt_triangle* tris, int32_t n, pt_bvh_node*
                                 int32_t* num_nodes, int32_t* tri_indices) {
     int32_t rc = PT_OK;
     pt_triangle* d_tris = nullptr;
-    int *d_idx = nullptr, *d_idx2 = nullptr, *d_J = nullptr, *d_Jn = nullptr, *d_nl = nullptr;
-    Seg* d_segs = nullptr;
-    float* d_bounds = nullptr;
+    int *d_idx = nullptr, *d_idx2 = nullptr, *d_J = nullptr, *d_Jn = nullptr;
+    unsigned char* d_less = nullptr;
+    // per-level scratch, grown on demand
+    Piece* d_pieces = nullptr;
+    int *d_first = nullptr, *d_pf = nullptr, *d_cnt = nullptr, *d_nless = nullptr, *d_sstart = nullptr;
+    float *d_pv = nullptr, *d_bounds = nullptr;
+    Split* d_splits = nullptr;
+    size_t piece_cap = 0, seg_cap = 0, small_cap = 0;
+    const bool timing = getenv("PT_BVH_TIMING") != nullptr;   // per-level times on stderr (tools)
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    std::chrono::steady_clock::time_point t_start = clk();
+    SmallSeg* d_small = nullptr;
+    Split* d_ssplit = nullptr;
+    int* d_snless = nullptr;
     int dev_count = 0;
     std::vector<TreeNode> tree;
     std::vector<int> level;   // skeleton indices of the current level
     std::vector<int> pre;
-    size_t seg_cap = 0;
+    const unsigned gn = (unsigned)((n + BT - 1) / BT);
     if (n < 0 || !num_nodes || (n > 0 && (!tris || !nodes || !tri_indices))) {
         g_err = "bad arguments";
         return PT_E_INVALID;
@@ -276,6 +395,7 @@ extern "C" int32_t pt_bvh_build(const pt_triangle* tris, int32_t n, pt_bvh_node*
     BCHK(hipMalloc(&d_idx2, sizeof(int) * (size_t)n));
     BCHK(hipMalloc(&d_J, sizeof(int) * (size_t)n));
     BCHK(hipMalloc(&d_Jn, sizeof(int) * (size_t)n));
+    BCHK(hipMalloc(&d_less, (size_t)n));
     BCHK(hipMemcpy(d_tris, tris, sizeof(pt_triangle) * (size_t)n, hipMemcpyHostToDevice));
     {
         std::vector<int> iota(n);
@@ -283,66 +403,166 @@ extern "C" int32_t pt_bvh_build(const pt_triangle* tris, int32_t n, pt_bvh_node*
         BCHK(hipMemcpy(d_idx, iota.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
     }
     tree.push_back(TreeNode{0, n});
+    tree.reserve(2 * (size_t)n);
     level.push_back(0);
+    t_start = clk();
     while (!level.empty()) {
-        const size_t S = level.size();
-        if (S > seg_cap) {
-            (void)hipFree(d_segs);
-            (void)hipFree(d_bounds);
-            (void)hipFree(d_nl);
-            d_segs = nullptr;
-            d_bounds = nullptr;
-            d_nl = nullptr;
-            seg_cap = std::max<size_t>(S, 2 * seg_cap);
-            BCHK(hipMalloc(&d_segs, sizeof(Seg) * seg_cap));
-            BCHK(hipMalloc(&d_bounds, sizeof(float) * 12 * seg_cap));
-            BCHK(hipMalloc(&d_nl, sizeof(int) * seg_cap));
-        }
-        std::vector<Seg> segs(S);
-        for (size_t s = 0; s < S; ++s) segs[s] = Seg{tree[level[s]].start, tree[level[s]].end, 0, 0.f};
-        BCHK(hipMemcpy(d_segs, segs.data(), sizeof(Seg) * S, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(k_seg_bounds, dim3((unsigned)S), dim3(BT), 0, 0, d_tris, d_idx, d_segs, d_bounds);
-        BCHK(hipGetLastError());
-        std::vector<float> bounds(12 * S);
-        BCHK(hipMemcpy(bounds.data(), d_bounds, sizeof(float) * 12 * S, hipMemcpyDeviceToHost));
-        // split decisions (scene.cpp:466-499) on the host: a few float ops per node
-        std::vector<Seg> split, leaf;
-        std::vector<int> split_node;
-        for (size_t s = 0; s < S; ++s) {
-            TreeNode& t = tree[level[s]];
-            memcpy(t.b, &bounds[12 * s], 6 * sizeof(float));
-            if (t.end - t.start <= 4) {
-                leaf.push_back(segs[s]);
+        auto t_lv = clk();
+        const int S = (int)level.size();
+        // pieces of every node of the level, in node order
+        std::vector<Piece> pieces;
+        std::vector<int> first(S + 1);
+        std::vector<SmallSeg> small;
+        for (int k = 0; k < S; ++k) {
+            first[k] = (int)pieces.size();
+            const TreeNode& t = tree[level[k]];
+            if (t.end - t.start <= SMALL) {
+                small.push_back(SmallSeg{k, t.start, t.end});
                 continue;
             }
-            const float* cmin = &bounds[12 * s + 6];
-            const float* cmax = &bounds[12 * s + 9];
+            for (int a = t.start; a < t.end; a += PIECE) pieces.push_back(Piece{k, a, std::min(t.end, a + PIECE)});
+        }
+        first[S] = (int)pieces.size();
+        if (pieces.size() > piece_cap) {
+            (void)hipFree(d_pieces);
+            (void)hipFree(d_pv);
+            (void)hipFree(d_pf);
+            (void)hipFree(d_cnt);
+            d_pieces = nullptr;
+            d_pv = nullptr;
+            d_pf = nullptr;
+            d_cnt = nullptr;
+            piece_cap = std::max(pieces.size(), 2 * piece_cap);
+            BCHK(hipMalloc(&d_pieces, sizeof(Piece) * piece_cap));
+            BCHK(hipMalloc(&d_pv, sizeof(float) * 12 * piece_cap));
+            BCHK(hipMalloc(&d_pf, sizeof(int) * 12 * piece_cap));
+            BCHK(hipMalloc(&d_cnt, sizeof(int) * piece_cap));
+        }
+        if (small.size() > small_cap) {
+            (void)hipFree(d_small);
+            (void)hipFree(d_ssplit);
+            (void)hipFree(d_snless);
+            d_small = nullptr;
+            d_ssplit = nullptr;
+            d_snless = nullptr;
+            small_cap = std::max(small.size(), 2 * small_cap);
+            BCHK(hipMalloc(&d_small, sizeof(SmallSeg) * small_cap));
+            BCHK(hipMalloc(&d_ssplit, sizeof(Split) * small_cap));
+            BCHK(hipMalloc(&d_snless, sizeof(int) * small_cap));
+        }
+        if ((size_t)S + 1 > seg_cap) {
+            (void)hipFree(d_first);
+            (void)hipFree(d_bounds);
+            (void)hipFree(d_nless);
+            (void)hipFree(d_sstart);
+            (void)hipFree(d_splits);
+            d_first = nullptr;
+            d_bounds = nullptr;
+            d_nless = nullptr;
+            d_sstart = nullptr;
+            d_splits = nullptr;
+            seg_cap = std::max<size_t>(S + 1, 2 * seg_cap);
+            BCHK(hipMalloc(&d_first, sizeof(int) * seg_cap));
+            BCHK(hipMalloc(&d_bounds, sizeof(float) * 12 * seg_cap));
+            BCHK(hipMalloc(&d_nless, sizeof(int) * seg_cap));
+            BCHK(hipMalloc(&d_sstart, sizeof(int) * seg_cap));
+            BCHK(hipMalloc(&d_splits, sizeof(Split) * seg_cap));
+        }
+        if (!pieces.empty()) {
+            BCHK(hipMemcpy(d_pieces, pieces.data(), sizeof(Piece) * pieces.size(), hipMemcpyHostToDevice));
+            BCHK(hipMemcpy(d_first, first.data(), sizeof(int) * (S + 1), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_piece_fold, dim3((unsigned)pieces.size()), dim3(BT), 0, 0, d_tris, d_idx, d_pieces,
+                               d_pv, d_pf);
+            hipLaunchKernelGGL(k_seg_fold, dim3((unsigned)((S + 3) / 4)), dim3(64), 0, 0, d_first, d_pv, d_pf, d_bounds,
+                               S);
+        }
+        if (!small.empty()) {   // after k_seg_fold, which writes the empty fold into small nodes' slots
+            BCHK(hipMemcpy(d_small, small.data(), sizeof(SmallSeg) * small.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_small_bounds, dim3((unsigned)((small.size() + 63) / 64)), dim3(64), 0, 0, d_tris,
+                               d_idx, d_small, d_bounds, (int)small.size());
+        }
+        BCHK(hipGetLastError());
+        std::vector<float> bounds(12 * (size_t)S);
+        BCHK(hipMemcpy(bounds.data(), d_bounds, sizeof(float) * 12 * S, hipMemcpyDeviceToHost));
+        // split decisions (scene.cpp:466-499) on the host: a few float ops per node
+        std::vector<int> split_nodes;                 // skeleton indices of the nodes that split
+        std::vector<Split> splits;
+        std::vector<Piece> spieces;                   // their pieces, seg = index into split_nodes
+        std::vector<int> sfirst{0}, sstart;
+        std::vector<int> small_nodes;                 // small nodes that split (thread per node)
+        std::vector<SmallSeg> ssegs;
+        std::vector<Split> ssplits;
+        for (int k = 0; k < S; ++k) {
+            TreeNode& t = tree[level[k]];
+            memcpy(t.b, &bounds[12 * (size_t)k], 6 * sizeof(float));
+            if (t.end - t.start <= 4) continue;
+            const float* cmin = &bounds[12 * (size_t)k + 6];
+            const float* cmax = &bounds[12 * (size_t)k + 9];
             const float ex = cmax[0] - cmin[0], ey = cmax[1] - cmin[1], ez = cmax[2] - cmin[2];
             int axis = 0;
             if (ey > ex && ey > ez) axis = 1;
             if (ez > ex) axis = 2;
-            const float sp = 0.5f * (cmin[axis] + cmax[axis]);
-            split.push_back(Seg{t.start, t.end, axis, sp});
-            split_node.push_back(level[s]);
+            if (t.end - t.start <= SMALL) {
+                small_nodes.push_back(level[k]);
+                ssegs.push_back(SmallSeg{k, t.start, t.end});
+                ssplits.push_back(Split{axis, 0.5f * (cmin[axis] + cmax[axis])});
+                continue;
+            }
+            const int si = (int)split_nodes.size();
+            split_nodes.push_back(level[k]);
+            splits.push_back(Split{axis, 0.5f * (cmin[axis] + cmax[axis])});
+            sstart.push_back(t.start);
+            for (int p = first[k]; p < first[k + 1]; ++p) spieces.push_back(Piece{si, pieces[p].start, pieces[p].end});
+            sfirst.push_back((int)spieces.size());
         }
-        std::vector<Seg> all(split);
-        all.insert(all.end(), leaf.begin(), leaf.end());
-        BCHK(hipMemcpy(d_segs, all.data(), sizeof(Seg) * all.size(), hipMemcpyHostToDevice));
-        if (!split.empty())
-            hipLaunchKernelGGL(k_seg_partition, dim3((unsigned)split.size()), dim3(BT), 0, 0, d_tris, d_idx, d_idx2,
-                               d_segs, d_J, d_Jn, d_nl);
-        if (!leaf.empty())
-            hipLaunchKernelGGL(k_seg_copy, dim3((unsigned)leaf.size()), dim3(BT), 0, 0, d_idx, d_idx2,
-                               d_segs + split.size());
+        const int SS = (int)split_nodes.size();
+        hipLaunchKernelGGL(k_fill, dim3(gn), dim3(BT), 0, 0, d_J, d_less, n);
+        std::vector<int> snl(small_nodes.size());
+        if (!small_nodes.empty()) {
+            BCHK(hipMemcpy(d_small, ssegs.data(), sizeof(SmallSeg) * ssegs.size(), hipMemcpyHostToDevice));
+            BCHK(hipMemcpy(d_ssplit, ssplits.data(), sizeof(Split) * ssplits.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(k_small_partition, dim3((unsigned)((ssegs.size() + 63) / 64)), dim3(64), 0, 0, d_tris,
+                               d_idx, d_idx2, d_small, d_ssplit, d_less, d_snless, (int)ssegs.size());
+            BCHK(hipGetLastError());
+            BCHK(hipMemcpy(snl.data(), d_snless, sizeof(int) * snl.size(), hipMemcpyDeviceToHost));
+        }
+        std::vector<int> nl(SS);
+        if (SS > 0) {
+            int maxlen = 0;
+            for (int k = 0; k < SS; ++k) maxlen = std::max(maxlen, tree[split_nodes[k]].end - tree[split_nodes[k]].start);
+            BCHK(hipMemcpy(d_pieces, spieces.data(), sizeof(Piece) * spieces.size(), hipMemcpyHostToDevice));
+            BCHK(hipMemcpy(d_first, sfirst.data(), sizeof(int) * (SS + 1), hipMemcpyHostToDevice));
+            BCHK(hipMemcpy(d_splits, splits.data(), sizeof(Split) * SS, hipMemcpyHostToDevice));
+            BCHK(hipMemcpy(d_sstart, sstart.data(), sizeof(int) * SS, hipMemcpyHostToDevice));
+            const unsigned np = (unsigned)spieces.size();
+            hipLaunchKernelGGL(k_piece_count, dim3(np), dim3(BT), 0, 0, d_tris, d_idx, d_pieces, d_splits, d_less,
+                               d_cnt);
+            hipLaunchKernelGGL(k_seg_scan, dim3((unsigned)((SS + 255) / 256)), dim3(256), 0, 0, d_first, d_cnt, d_nless,
+                               SS);
+            hipLaunchKernelGGL(k_piece_place, dim3(np), dim3(BT), 0, 0, d_idx, d_idx2, d_pieces, d_sstart, d_less,
+                               d_cnt, d_J);
+            int rounds = 1;
+            while ((1 << (rounds - 1)) < maxlen) ++rounds;   // ceil(log2 maxlen) + 1
+            for (int r = 0; r < rounds; ++r) {
+                hipLaunchKernelGGL(k_jump, dim3(gn), dim3(BT), 0, 0, d_J, d_Jn, n);
+                std::swap(d_J, d_Jn);
+            }
+            BCHK(hipGetLastError());
+            BCHK(hipMemcpy(nl.data(), d_nless, sizeof(int) * SS, hipMemcpyDeviceToHost));
+        }
+        hipLaunchKernelGGL(k_scatter_rest, dim3(gn), dim3(BT), 0, 0, d_idx, d_idx2, d_J, d_less, n);
         BCHK(hipGetLastError());
-        std::vector<int> nl(split.size());
-        if (!split.empty()) BCHK(hipMemcpy(nl.data(), d_nl, sizeof(int) * split.size(), hipMemcpyDeviceToHost));
         std::swap(d_idx, d_idx2);
+        // children in level order (big and small split nodes are interleaved in the level)
         std::vector<int> next;
-        for (size_t k = 0; k < split.size(); ++k) {
-            const int ti = split_node[k];
+        next.reserve(2 * (split_nodes.size() + small_nodes.size()));
+        size_t ib = 0, is = 0;
+        while (ib < split_nodes.size() || is < small_nodes.size()) {
+            const bool big = is >= small_nodes.size() || (ib < split_nodes.size() && split_nodes[ib] < small_nodes[is]);
+            const int ti = big ? split_nodes[ib] : small_nodes[is];
+            const int nlk = big ? nl[ib++] : snl[is++];
             const int st = tree[ti].start, en = tree[ti].end;
-            int mid = st + nl[k];
+            int mid = st + nlk;
             if (mid == st || mid == en) mid = (st + en) / 2;   // scene.cpp:513-515
             const int l = (int)tree.size();
             tree.push_back(TreeNode{st, mid});
@@ -353,8 +573,17 @@ extern "C" int32_t pt_bvh_build(const pt_triangle* tris, int32_t n, pt_bvh_node*
             next.push_back(l + 1);
         }
         level.swap(next);
+        if (timing) {
+            BCHK(hipDeviceSynchronize());
+            const double ms = std::chrono::duration<double, std::milli>(clk() - t_lv).count();
+            std::fprintf(stderr, "pt_bvh_build level: %zu nodes (%d split, %zu small) %.3f ms\n", (size_t)S, SS,
+                         small_nodes.size(), ms);
+        }
     }
     BCHK(hipDeviceSynchronize());
+    if (timing)
+        std::fprintf(stderr, "pt_bvh_build levels total %.3f ms\n",
+                     std::chrono::duration<double, std::milli>(clk() - t_start).count());
     BCHK(hipMemcpy(tri_indices, d_idx, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost));
     {
         // preorder numbering (the reference pushes a node, then recurses left, then right)
@@ -387,13 +616,9 @@ extern "C" int32_t pt_bvh_build(const pt_triangle* tris, int32_t n, pt_bvh_node*
         *num_nodes = T;
     }
 done:
-    (void)hipFree(d_tris);
-    (void)hipFree(d_idx);
-    (void)hipFree(d_idx2);
-    (void)hipFree(d_J);
-    (void)hipFree(d_Jn);
-    (void)hipFree(d_segs);
-    (void)hipFree(d_bounds);
-    (void)hipFree(d_nl);
+    for (void* q : {(void*)d_tris, (void*)d_idx, (void*)d_idx2, (void*)d_J, (void*)d_Jn, (void*)d_less,
+                    (void*)d_pieces, (void*)d_first, (void*)d_pf, (void*)d_cnt, (void*)d_nless, (void*)d_sstart,
+                    (void*)d_pv, (void*)d_bounds, (void*)d_splits, (void*)d_small, (void*)d_ssplit, (void*)d_snless})
+        (void)hipFree(q);
     return rc;
 }
