@@ -1043,9 +1043,11 @@ struct BlockLds {
     uint16_t task[BCAP];
     int wsum[BLOCK / 64];
 };
+template <bool TIMING = false>
 PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, BlockLds* B,
                             float& t_min, int& win, f3& seed) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t tc0 = TIMING ? sec_clock() : 0;
     uint64_t cand = 0;
     CullRay cr;
     if (live) {
@@ -1057,6 +1059,12 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
             if (cull_keep(sc, i, cr, ro, rd, bounded)) cand |= 1ull << i;
     }
     const int cnt = __builtin_popcountll(cand);
+    uint64_t tc1 = 0;
+    if (TIMING) {
+        tc1 = sec_clock();
+        sec_add(SEC_CULL, tc1 - tc0);
+        sec_add_lanes(SEC_N_CAND, cnt);
+    }
     int incl = cnt;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1126,6 +1134,10 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
             win = B->task[j] & 255;
             seed = mk(B->rs[0][j], B->rs[1][j], B->rs[2][j]);
         }
+    }
+    if (TIMING) {
+        sec_add(SEC_EXACT, sec_clock() - tc1);
+        sec_add_lanes(SEC_N_EXACT, cnt);
     }
 }
 

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -239,8 +240,8 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     f3 qs = mk(0.f, 0.f, 0.f);
     if (REDIST && lds_geoms) {                     // wave-cooperative: every lane takes part
         if (VAR & VAR_BLOCK_REDIST)
-            block_intersect(sc, s_geoms, live, p.o, p.d, reinterpret_cast<BlockLds*>(s_wave_isect - (tid >> 6)), qt,
-                            qw, qs);
+            block_intersect<TIMING>(sc, s_geoms, live, p.o, p.d, reinterpret_cast<BlockLds*>(s_wave_isect - (tid >> 6)),
+                                    qt, qw, qs);
         else
             wave_intersect<TIMING>(sc, s_geoms, live, p.o, p.d, s_wave_isect, qt, qw, qs);
     } else if (SPLIT && live) {
@@ -872,6 +873,7 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 154: launch_bounce_t<FIRST, HAS_BVH, 154>(grid, in, out, b); break;
         case 186: launch_bounce_t<FIRST, HAS_BVH, 186>(grid, in, out, b); break;
         case 190: launch_bounce_t<FIRST, HAS_BVH, 190>(grid, in, out, b); break;   // 186 + section counters
+        case 158: launch_bounce_t<FIRST, HAS_BVH, 158>(grid, in, out, b); break;   // 154 + section counters
         case 442: launch_bounce_t<FIRST, HAS_BVH, 442>(grid, in, out, b); break;   // 186 + 4-wide BVH
         case 446: launch_bounce_t<FIRST, HAS_BVH, 446>(grid, in, out, b); break;   // 442 + section counters
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
@@ -881,6 +883,9 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     // camera rays of neighbouring pixels share their candidates: redistribution only costs there
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
+    // tools: PT_SECTIONS_SKIP_CAMERA=1 leaves the camera bounce out of the section counters
+    static const bool skip_cam = getenv("PT_SECTIONS_SKIP_CAMERA") != nullptr;
+    if (first && skip_cam) var &= ~VAR_SECTION_TIMING;
     if (!g.split) var &= ~VAR_BVH_SPLIT;
     if (!g.sc.quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
     if (first) {
