@@ -86,8 +86,9 @@ typedef struct pt_options {
                                     128: with 8, the exact-test exchange spans the whole block);
                                     results are bit-identical for every value.  Default
                                     2|8|16|32|128 */
-    int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..32;
-                                    0 = auto: ~21M paths in flight).  The image is bit-identical
+    int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..256;
+                                    0 = auto: ~21M paths in flight, e.g. 32 at 800x800, 256 for
+                                    a 1/8 pixel shard of it).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in
                                     per-frame planes that are added in frame order. */
 } pt_options;

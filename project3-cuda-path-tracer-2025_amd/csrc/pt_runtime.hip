@@ -730,7 +730,7 @@ int dalloc(T** p, size_t n) {
     return PT_OK;
 }
 
-constexpr int MAXF = 32;                    // frames per pass, upper bound
+constexpr int MAXF = 256;                   // frames per pass, upper bound (slot: 8 bits of a queue entry)
 // auto F: up to ~21M paths at bounce 0 -> 800x800: F = 32, 1600x1600: F = 8.  A/B (ms/frame):
 // cornell 800^2 F = 8 0.0992, 16 0.0949 (0.0937), 32 0.0921; bunny 800^2 F = 8 0.685, 16 0.633;
 // khaslana 1600^2 F = 2 2.52, 4 1.95 (1.93), 8 1.66 (earlier kernels: F = 1 0.214, 2 0.161,
