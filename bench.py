@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[2..4] sub-records")
     ap.add_argument("--no-api", action="store_true", help="skip the single-frame pt_trace() timing")
+    ap.add_argument("--no-spread", action="store_true", help="skip the per-pass median / p90 timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=["pixels", "samples"], default="pixels",
                     help="N>1: pixels = interleaved row bands of every frame per rank (default); "
@@ -182,7 +183,7 @@ def main():
         tr.reset_stats()
         prof = tr.profile(it, args.steps)
         st_prof = tr.stats()
-        spread = pass_spread(tr, it + args.steps, st_prof["frames_per_pass"])
+        spread = None if args.no_spread else pass_spread(tr, it + args.steps, st_prof["frames_per_pass"])
     seen_world = world
     if world > 1:
         t = torch.tensor([elapsed, float(segs), t_comb], dtype=torch.float64,

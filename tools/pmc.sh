@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # rocprofv3 PMC passes (counters only with --kernel-trace/--stats, never with sys/runtime traces)
-# over a short bench run; each pass in its own process.  Usage: tools/pmc.sh [extra bench args]
+# over a short bench run (warmup 8 + 32 timed frames + bench's 32-frame profiling replay = 72 frames,
+# no sub-configs / api / spread runs); each pass in its own process.  Usage: tools/pmc.sh [extra bench args]
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -14,7 +15,7 @@ for set in "${SETARR[@]}"; do
     i=$((i+1))
     echo "== pass $i: $set"
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d "$OUT/${PMC_TAG:-}p$i" -o run --output-format csv -- \
-        python bench.py --steps ${PMC_STEPS:-32} --warmup ${PMC_WARMUP:-8} --no-cpu-baseline "$@" > "$OUT/${PMC_TAG:-}p$i.log" 2>&1
+        python bench.py --steps ${PMC_STEPS:-32} --warmup ${PMC_WARMUP:-8} --no-cpu-baseline --no-configs --no-api --no-spread "$@" > "$OUT/${PMC_TAG:-}p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ]; then tail -20 "$OUT/${PMC_TAG:-}p$i.log"; exit $rc; fi
