@@ -660,3 +660,26 @@ def test_deep_skewed_gpu_bvh(tmp_path, oracle, ptamd):
     h = ptamd.SceneFile(path, viewer_camera=False)
     g = ptamd.SceneFile(path, viewer_camera=False, gpu_bvh=True)
     assert g.bvh_nodes.tobytes() == h.bvh_nodes.tobytes() and g.tri_indices.tobytes() == h.tri_indices.tobytes()
+
+
+def test_bench_four_ranks_config5_shape(tmp_path, oracle):
+    """BASELINE configs[4]'s shape (khaslana, depth 12, pixel tiles + tile gather) with 4 ranks
+    sharing this GPU (gloo) at 160x160: `bench.py --gpus 4` traces 4 x (W + K) frames over the
+    ranks' row bands, rank 0 gathers the tiles; bit-identical to the oracle's frames."""
+    dump = tmp_path / "img.npy"
+    env = dict(os.environ, PT_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--scene",
+                        scene_path("cornell_obj_khaslana"), "--res", "160x160", "--depth", "12", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-configs", "--no-api", "--dump-image", str(dump)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 4 and line["distributed"]["world_size"] == 4
+    a = oracle.load_scene(scene_path("cornell_obj_khaslana"), res=(160, 160), depth=12)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in range(1, 4 * (1 + 2) + 1):
+        r.trace(it)
+    got = np.load(dump)
+    assert _eq(got, r.image), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
