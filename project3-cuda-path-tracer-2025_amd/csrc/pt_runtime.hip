@@ -851,9 +851,11 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
     launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + redist_lds, g.sc, in, out,
            g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
+    // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
+    static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds, g.sc, g.queue, out, g.d_ctl, g.d_image, b,
-               g.seg_stride);
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds + lds_pad, g.sc, g.queue, out, g.d_ctl,
+               g.d_image, b, g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -876,10 +878,15 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 158: launch_bounce_t<FIRST, HAS_BVH, 158>(grid, in, out, b); break;   // 154 + section counters
         case 442: launch_bounce_t<FIRST, HAS_BVH, 442>(grid, in, out, b); break;   // 186 + 4-wide BVH
         case 446: launch_bounce_t<FIRST, HAS_BVH, 446>(grid, in, out, b); break;   // 442 + section counters
-        default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;
+        case 306: launch_bounce_t<FIRST, HAS_BVH, 306>(grid, in, out, b); break;   // camera bounce of 442
+        case 310: launch_bounce_t<FIRST, HAS_BVH, 310>(grid, in, out, b); break;   // camera bounce of 446
+        default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;   // unreachable: pt_init checks
     }
 }
-void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
+// the fused kernel's template variant for a bounce: the requested bits minus what this bounce /
+// scene does not use
+int effective_variant(bool first, int var, bool has_quads) {
+    var &= ~VAR_BVH_NODES;   // host-only bit (layout choice)
     // camera rays of neighbouring pixels share their candidates: redistribution only costs there
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
@@ -887,7 +894,19 @@ void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf
     static const bool skip_cam = getenv("PT_SECTIONS_SKIP_CAMERA") != nullptr;
     if (first && skip_cam) var &= ~VAR_SECTION_TIMING;
     if (!g.split) var &= ~VAR_BVH_SPLIT;
-    if (!g.sc.quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
+    if (!has_quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
+    return var;
+}
+// variants instantiated in launch_bounce_v (pt_init refuses others instead of running a
+// different kernel than asked for)
+bool variant_compiled(int v) {
+    static const int k[] = {0, 1, 2, 6, 10, 18, 22, 26, 30, 50, 54, 58, 154, 158, 186, 190, 306, 310, 442, 446};
+    for (int x : k)
+        if (x == v) return true;
+    return false;
+}
+void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
+    var = effective_variant(first, var, g.sc.quads != nullptr);
     if (first) {
         if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
         else launch_bounce_v<true, false>(var, grid, in, out, b);
@@ -1669,6 +1688,14 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     g.split = g.has_bvh && !pairs.empty() && o.pipeline == PT_PIPELINE_FUSED && (o.variant & VAR_BVH_SPLIT) &&
               (o.variant & VAR_BVH_FAST) && (o.variant & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) &&
               s->num_geoms <= LDS_GEOMS;
+    if (o.pipeline == PT_PIPELINE_FUSED) {
+        for (int first = 0; first < 2; ++first) {
+            const int v = effective_variant(first != 0, o.variant, !quads.empty());
+            if (v != 3 && !variant_compiled(v))
+                return fail(PT_E_UNSUPPORTED, "variant %d (effective %d for the %s bounce) is not compiled in", o.variant,
+                            v, first ? "camera" : "later");
+        }
+    }
     const int nb = nblocks(std::max(1, g.local_pixels * g.batch));
     // output segment s receives the survivors of the chunks c = s (mod NSEG): of k_bounce's, and
     // in split mode also of k_bvh_bounce's (its chunks of the queue) -- twice the room then
