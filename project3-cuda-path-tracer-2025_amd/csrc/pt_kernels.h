@@ -267,6 +267,26 @@ PT_DEV bool aabb_decide(float4 lo, float4 hi, f3 ro, f3 rd, f3 rr, bool exact, f
     }
     return aabb_test(lo, hi, ro, rd);
 }
+// aabb_decide for a ray that is finite with every |d| >= 1e-5 (no per-axis "parallel" branch,
+// no exact-mode branch): the same slab values, max / min taken in another association (exact
+// operations, no NaN can arise), the same certain-pass / certain-fail thresholds.  `amb` is set
+// when neither is certain; the caller then asks aabb_test (the reference arithmetic).
+PT_DEV bool aabb_fast(float4 lo, float4 hi, f3 ro, f3 rr, float& entry, bool& amb) {
+    const float t1x = (lo.x - ro.x) * rr.x, t2x = (hi.x - ro.x) * rr.x;
+    const float t1y = (lo.y - ro.y) * rr.y, t2y = (hi.y - ro.y) * rr.y;
+    const float t1z = (lo.z - ro.z) * rr.z, t2z = (hi.z - ro.z) * rr.z;
+    const float tmin = __builtin_fmaxf(__builtin_fmaxf(-FLT_MAX_, __builtin_fminf(t1x, t2x)),
+                                       __builtin_fmaxf(__builtin_fminf(t1y, t2y), __builtin_fminf(t1z, t2z)));
+    const float tmax = __builtin_fminf(__builtin_fminf(FLT_MAX_, __builtin_fmaxf(t1x, t2x)),
+                                       __builtin_fminf(__builtin_fmaxf(t1y, t2y), __builtin_fmaxf(t1z, t2z)));
+    entry = tmin;
+    const float e = 1e-6f * (__builtin_fabsf(tmin) + __builtin_fabsf(tmax));
+    const bool pos = tmax > 0.f;
+    const bool yes = pos & (tmax - tmin > e);
+    const bool no = !pos | (tmin - tmax > e);
+    amb = !(yes | no);
+    return yes;
+}
 PT_DEV bool node_culled(float entry, float4 aux, float t_best) {
     if (!(entry > 0.0f)) return false;
     const float rho = aux.x * (2.0f + aux.y * __builtin_amdgcn_rcpf(t_best) * 1.001f) + 1e-6f;
@@ -381,90 +401,126 @@ struct TravState {
     f3 ro, rd, rr;
     float t_limit, t_hit, bu, bv;
     int btri, cur, sp;
+    float curT;   // certified cull threshold of st.cur (0: none)
     bool exact;
+    bool wfast;   // wave-uniform: every ray of the wave is finite with all |d| >= 1e-5 (aabb_fast)
 };
 PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_limit) {
     st.ro = ro;
     st.rd = rd;
     st.exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
                  rd.x - rd.x == 0.f && rd.y - rd.y == 0.f && rd.z - rd.z == 0.f);   // NaN / inf ray
+    const bool par = __builtin_fabsf(rd.x) < 0.00001f || __builtin_fabsf(rd.y) < 0.00001f ||
+                     __builtin_fabsf(rd.z) < 0.00001f;
+    st.wfast = __all(!(st.exact || par));
     st.rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
     st.t_limit = t_limit;
     st.t_hit = FLT_MAX_;
     st.bu = st.bv = 0.f;
     st.btri = 0x7fffffff;
     st.sp = 0;
+    st.curT = 0.f;
     float e0;
     st.cur = (aabb_decide(sc.root_lo, sc.root_hi, ro, rd, st.rr, st.exact, e0) &&
               !(t_limit < cull_threshold(sc, e0, sc.root_hi.w)))
                  ? sc.root_ref
                  : -1;
 }
+// pop the nearest stack entry whose certified cull does not reject it (st.cur = -1: empty)
+PT_DEV void trav_pop(TravState& st, int* stack) {
+    const float tb = __builtin_fminf(st.t_hit, st.t_limit);
+    st.cur = -1;
+    while (st.sp > 0) {
+        const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
+        const float T = __uint_as_float(w << 16);
+        if (!(tb < T)) {
+            st.cur = (int)(w >> 16);
+            st.curT = T;
+            break;
+        }
+    }
+}
+// expand the internal node st.cur: both child boxes decided exactly (aabb_fast / aabb_decide),
+// certified culls, the nearer passing child continues (true) and the farther one is pushed;
+// false: no child passes (the caller pops)
+template <bool COUNT = false>
+PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
+    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
+    if (COUNT) n_nodes++;
+    const DevPair pr = sc.pairs[st.cur];
+    float el = 0.f, er = 0.f;
+    bool pl, pb;
+    if (st.wfast) {   // wave-uniform
+        bool al, ar;
+        pl = aabb_fast(pr.l_lo, pr.l_hi, st.ro, st.rr, el, al);
+        pb = aabb_fast(pr.r_lo, pr.r_hi, st.ro, st.rr, er, ar);
+        if (al | ar) {   // rare: a gap within the rcp slabs' error, the reference decides
+            if (al) pl = aabb_test(pr.l_lo, pr.l_hi, st.ro, st.rd);
+            if (ar) pb = aabb_test(pr.r_lo, pr.r_hi, st.ro, st.rd);
+        }
+    } else {
+        pl = aabb_decide(pr.l_lo, pr.l_hi, st.ro, st.rd, st.rr, st.exact, el);
+        pb = aabb_decide(pr.r_lo, pr.r_hi, st.ro, st.rd, st.rr, st.exact, er);
+    }
+    const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
+    const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
+    pl = pl && !(t_best < Tl);
+    pb = pb && !(t_best < Tr);
+    const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
+    if (pl && pb) {
+        const bool lfirst = el <= er;
+        st.cur = lfirst ? rl : rrf;
+        st.curT = lfirst ? Tl : Tr;
+        const int far = lfirst ? rrf : rl;
+        const float Tf = lfirst ? Tr : Tl;
+        if (st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
+        return true;
+    }
+    if (pl | pb) {
+        st.cur = pl ? rl : rrf;
+        st.curT = pl ? Tl : Tr;
+        return true;
+    }
+    return false;
+}
+// test the 4 slots of leaf `leaf` (ref - num_pairs): 9 float4, component k of slots 0..3, the
+// edges v1 - v0, v2 - v0 precomputed (same float rounding).  Unused slots are all-zero (det = 0:
+// rejected; a NaN ray gets t = NaN, which `t > 0` never accepts).  Ties on t go to the smaller
+// slot (the reference's visit order), so the order leaves are tested in does not matter.
+template <bool COUNT = false>
+PT_DEV void trav_leaf(const SceneDev& sc, TravState& st, int leaf, int& n_nodes, int& n_tris) {
+    const int base = 4 * leaf;
+    if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
+    const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
+    v4f c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = L[k];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
+        const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
+        const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
+        float t, u, v;
+        if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
+            (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
+            st.t_hit = t;
+            st.bu = u;
+            st.bv = v;
+            st.btri = base + i;
+        }
+    }
+}
 // one node expansion or one leaf; st.cur < 0 afterwards: the ray is finished
 template <bool COUNT = false>
 PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
     const int P = sc.num_pairs;
-    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
-    const int cur = st.cur;
     bool next = false;
-    if (cur < P) {
-        if (COUNT) n_nodes++;
-        const DevPair pr = sc.pairs[cur];
-        float el = 0.f, er = 0.f;
-        bool pl = aabb_decide(pr.l_lo, pr.l_hi, st.ro, st.rd, st.rr, st.exact, el);
-        bool pb = aabb_decide(pr.r_lo, pr.r_hi, st.ro, st.rd, st.rr, st.exact, er);
-        const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
-        const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
-        pl = pl && !(t_best < Tl);
-        pb = pb && !(t_best < Tr);
-        const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
-        if (pl && pb) {
-            const bool lfirst = el <= er;
-            st.cur = lfirst ? rl : rrf;
-            const int far = lfirst ? rrf : rl;
-            const float Tf = lfirst ? Tr : Tl;
-            if (st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
-            next = true;
-        } else if (pl | pb) {
-            st.cur = pl ? rl : rrf;
-            next = true;
-        }
+    if (st.cur < P) {
+        next = trav_inner<COUNT>(sc, st, stack, n_nodes);
     } else {
-        // the leaf's 4 slots as 9 float4 (component k of slots 0..3): 9 dwordx4 loads, and the
-        // edges v1 - v0, v2 - v0 come precomputed (same float rounding).  Unused slots are
-        // all-zero (det = 0: rejected; a NaN ray gets t = NaN, which `t > 0` never accepts).
-        const int leaf = cur - P, base = 4 * leaf;
-        if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
-        const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
-        v4f c[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) c[k] = L[k];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
-            const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
-            const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
-            float t, u, v;
-            if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
-                (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
-                st.t_hit = t;
-                st.bu = u;
-                st.bv = v;
-                st.btri = base + i;
-            }
-        }
+        trav_leaf<COUNT>(sc, st, st.cur - P, n_nodes, n_tris);
     }
-    if (!next) {
-        const float tb = __builtin_fminf(st.t_hit, st.t_limit);
-        st.cur = -1;
-        while (st.sp > 0) {
-            const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
-            if (!(tb < __uint_as_float(w << 16))) {
-                st.cur = (int)(w >> 16);
-                break;
-            }
-        }
-    }
+    if (!next) trav_pop(st, stack);
 }
 // result of a finished traversal: t (-1: no triangle), u, v, hot4 slot (-1)
 PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
@@ -908,27 +964,47 @@ PT_DEV bool certain_exact_miss(const DevGeom& g, f3 ro, f3 rd, bool bounded) {
     const int a = g.away_axis;
     return g.type == PT_CUBE && (unsigned)a < 3u && bounded && away_on_axis(g, a, ro, rd);
 }
-// !cull_geom<false>(g) && !certain_exact_miss(g) from geom i's DevCull record, its three loads
-// issued together ahead of any branch: same slab arithmetic as cull_geom, same qo / u arithmetic
-// as away_on_axis (only for records with an away row, on the lanes the box test kept)
-PT_DEV bool cull_keep(const SceneDev& sc, int i, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
-    const float4* rec = reinterpret_cast<const float4*>(sc.cull) + 3 * i;
-    const float4 A = rec[0], B = rec[1], C = rec[2];   // lo.xyz hi.x | hi.yz row0 row1 | row2 row3 - -
-    const float a0 = __builtin_fmaf(A.x, cr.id.x, -cr.rid.x), b0 = __builtin_fmaf(A.w, cr.id.x, -cr.rid.x);
-    const float a1 = __builtin_fmaf(A.y, cr.id.y, -cr.rid.y), b1 = __builtin_fmaf(B.x, cr.id.y, -cr.rid.y);
-    const float a2 = __builtin_fmaf(A.z, cr.id.z, -cr.rid.z), b2 = __builtin_fmaf(B.y, cr.id.z, -cr.rid.z);
-    const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
-                                     __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
-    const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
-                                     __builtin_fmaxf(a2, b2));
-    bool keep = t1 >= t0;
-    if (__float_as_int(C.z) != 0 && keep) {   // a record with an away row, lanes still keeping it
-        const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
-        const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
-        const bool away = (qo > 0.5f && u > 0.0f) || (qo < -0.5f && u < 0.0f);
-        keep = keep && !(bounded && away);
+// !cull_geom<false>(g) && !certain_exact_miss(g) for every geom, from the DevCull records (same
+// slab arithmetic as cull_geom, same qo / u arithmetic as away_on_axis), as a candidate mask
+// (bit i = geom i).  Records are read four geoms
+// (12 float4, 192 B) at a time, all loads of a group issued before any arithmetic, and the
+// away row is evaluated without a branch (all-zero rows are never "away"), so a group costs
+// one scalar-memory round trip instead of two per geom.  The host pads the record array to a
+// multiple of 4; bits of pad records are masked off by the (wave-uniform) index test.
+#ifndef CULL_GROUP
+#define CULL_GROUP 2
+#endif
+PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
+    const float4* rec = reinterpret_cast<const float4*>(sc.cull);
+    const int ng = sc.num_geoms;
+    uint64_t cand = 0;
+    for (int i0 = 0; i0 < ng; i0 += CULL_GROUP) {
+        float4 R[3 * CULL_GROUP];
+#pragma unroll
+        for (int k = 0; k < 3 * CULL_GROUP; ++k) R[k] = rec[3 * i0 + k];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < CULL_GROUP; ++k) {
+            const float4 A = R[3 * k], B = R[3 * k + 1], C = R[3 * k + 2];
+            const float a0 = __builtin_fmaf(A.x, cr.id.x, -cr.rid.x), b0 = __builtin_fmaf(A.w, cr.id.x, -cr.rid.x);
+            const float a1 = __builtin_fmaf(A.y, cr.id.y, -cr.rid.y), b1 = __builtin_fmaf(B.x, cr.id.y, -cr.rid.y);
+            const float a2 = __builtin_fmaf(A.z, cr.id.z, -cr.rid.z), b2 = __builtin_fmaf(B.y, cr.id.z, -cr.rid.z);
+            const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                             __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
+            const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                             __builtin_fmaxf(a2, b2));
+            const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
+            const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
+            // bitwise, not short-circuit: the compiler would otherwise branch around the away row
+            const uint32_t away = ((uint32_t)(qo > 0.5f) & (uint32_t)(u > 0.0f)) |
+                                  ((uint32_t)(qo < -0.5f) & (uint32_t)(u < 0.0f));
+            const uint32_t drop = away & (uint32_t)bounded & (uint32_t)(__float_as_int(C.z) != 0);
+            const uint32_t keep = (uint32_t)(t1 >= t0) & (drop ^ 1u) & (uint32_t)(i0 + k < ng);
+            bits |= keep << k;
+        }
+        cand |= (uint64_t)bits << i0;
     }
-    return keep;
+    return cand;
 }
 
 constexpr int WCAP = 192;      // pairs per wave held in LDS; more -> per-lane queue fallback
@@ -950,9 +1026,7 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
         // with the same arithmetic, so they take no slot in the exchanged exact tests
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
-#pragma unroll 4
-        for (int i = 0; i < sc.num_geoms; ++i)
-            if (cull_keep(sc, i, cr, ro, rd, bounded)) cand |= 1ull << i;
+        cand = cull_candidates(sc, cr, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;
@@ -1054,9 +1128,7 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
         cr = cull_ray(ro, rd);
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
-#pragma unroll 4
-        for (int i = 0; i < sc.num_geoms; ++i)
-            if (cull_keep(sc, i, cr, ro, rd, bounded)) cand |= 1ull << i;
+        cand = cull_candidates(sc, cr, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);
     uint64_t tc1 = 0;
