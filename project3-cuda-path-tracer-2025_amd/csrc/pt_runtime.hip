@@ -1514,6 +1514,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             c.dpdu[0] = t.dpdu.x; c.dpdu[1] = t.dpdu.y; c.dpdu[2] = t.dpdu.z;
             c.dpdv[0] = t.dpdv.x; c.dpdv[1] = t.dpdv.y; c.dpdv[2] = t.dpdv.z;
             c.materialID = t.materialID;
+            if (t.materialID < 0 || t.materialID >= std::max(1, s->num_materials))
+                return fail(PT_E_INVALID, "triangle %d material %d out of range", i, t.materialID);
         }
         // traversal stack (LDS, MAXSTACK entries per lane at most).  The reference-order DFS needs
         // bvh_max_stack entries -- more than 64 overflows the reference's own int stack[64]

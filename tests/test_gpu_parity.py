@@ -683,3 +683,18 @@ def test_bench_four_ranks_config5_shape(tmp_path, oracle):
         r.trace(it)
     got = np.load(dump)
     assert _eq(got, r.image), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
+
+
+def test_triangle_material_out_of_range_refused(ptamd):
+    """A triangle whose materialID names no material is refused at pt_init (PT_E_INVALID), as a
+    geom's is: the reference would index past its material array (pathtrace.cu:545)."""
+    sc = ptamd.SceneFile(scene_path("cornell_obj_bnnuy"), res=(16, 16), depth=2)
+    tris = sc.triangles.copy()
+    tris["materialID"][7] = len(sc.materials)
+    v = ptamd.scene_view_from_arrays(sc.geoms, sc.materials, sc.camera, 2, tris, sc.tri_indices, sc.bvh_nodes)
+    with pytest.raises(ptamd.PtError, match="triangle 7 material"):
+        ptamd.PathTracer(v)
+    ok = ptamd.PathTracer(ptamd.scene_view_from_arrays(sc.geoms, sc.materials, sc.camera, 2, sc.triangles,
+                                                       sc.tri_indices, sc.bvh_nodes))
+    ok.trace(1)
+    ok.free()
