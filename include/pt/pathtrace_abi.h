@@ -147,6 +147,13 @@ int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats);
 /* Overwrite the accumulated image (host data), e.g. after a multi-GPU reduce. */
 int32_t pt_set_image(const float* host_in, int64_t n_floats);
 
+/* Device memory for callers without the HIP headers (a PBO for pt_trace's pbo_device, as the
+ * headless viewer of pt/pt_viewer.h uses): hipMalloc / hipFree / synchronous hipMemcpy D->H
+ * (after the library's stream drained).  pt_device_alloc fails with PT_E_NODEVICE without a GPU. */
+int32_t pt_device_alloc(int64_t bytes, void** out);
+int32_t pt_device_free(void* p);
+int32_t pt_device_read(void* host_dst, const void* device_src, int64_t bytes);
+
 int32_t pt_get_frame_stats(pt_frame_stats* out);
 /* Zero the running totals of pt_frame_stats (frames_total, live_total, segments_total). */
 int32_t pt_reset_stats(void);

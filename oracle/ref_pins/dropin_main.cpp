@@ -48,9 +48,11 @@ int main(int argc, char** argv) {
     while (true) {   // runCuda, main.cpp:421-475
         if (camchanged) {
             iteration = 0;
-            cameraPosition.x = zoom * sin(phi) * sin(theta);
-            cameraPosition.y = zoom * cos(theta);
-            cameraPosition.z = zoom * cos(phi) * sin(theta);
+            // float overloads, as MSVC's <cmath> gives main.cpp's unqualified calls (the reference
+            // was built on Windows 10, README.md:19); g++ alone would pick ::sin(double)
+            cameraPosition.x = zoom * std::sin(phi) * std::sin(theta);
+            cameraPosition.y = zoom * std::cos(theta);
+            cameraPosition.z = zoom * std::cos(phi) * std::sin(theta);
             cam.view = -glm::normalize(cameraPosition);
             glm::vec3 v = cam.view;
             glm::vec3 u = glm::vec3(0, 1, 0);

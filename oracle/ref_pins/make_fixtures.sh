@@ -47,3 +47,17 @@ if [ -f "$CUDAINC/cuda_runtime.h" ] && [ -f "$PKGDIR/build/libptamd.so" ]; then
         -o "$OUT/dropin_main"
     echo "drop-in caller built: $OUT/dropin_main"
 fi
+# viewer_pin: main.cpp's camera controls restated on the reference's own Scene (scene.cpp) and glm,
+# replaying tests/golden/viewer_events.txt -> tests/golden/viewer_pin.json (headless viewer, pt_viewer.h)
+if [ -f "$CUDAINC/cuda_runtime.h" ]; then
+    g++ -std=c++17 -O2 -ffp-contract=off -w -I "$CUDAINC" -I "$REF/src" -I "$REF/external/include" \
+        "$HERE/viewer_pin.cpp" "$REF/src/scene.cpp" "$REF/src/utilities.cpp" "$REF/src/stb.cpp" -o "$OUT/viewer_pin"
+    {
+        echo '{"events": "viewer_events.txt", "scenes": {'
+        echo '"cornell.json": '; "$OUT/viewer_pin" "$REF/scenes/cornell.json" "$GOLD/viewer_events.txt" | sed -n '/^{"frames"/,$p'
+        echo ', "viewer_scene.json": '; "$OUT/viewer_pin" "$GOLD/viewer_scene.json" "$GOLD/viewer_events.txt" | sed -n '/^{"frames"/,$p'
+        echo '}}'
+    } | python3 -c 'import json, sys; json.dump(json.load(sys.stdin), sys.stdout, separators=(",", ":"))' \
+        > "$GOLD/viewer_pin.json"
+    echo "viewer fixtures: $GOLD/viewer_pin.json"
+fi

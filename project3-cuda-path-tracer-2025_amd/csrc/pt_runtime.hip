@@ -1939,6 +1939,28 @@ int32_t pt_set_image(const float* host_in, int64_t n_floats) {
     return PT_OK;
 }
 
+// device buffers for callers without the HIP headers (the headless viewer's PBO, ctypes)
+int32_t pt_device_alloc(int64_t bytes, void** out) {
+    if (!out || bytes <= 0) return fail(PT_E_INVALID, "pt_device_alloc: bad argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
+    HIPCHK(hipMalloc(out, (size_t)bytes));
+    return PT_OK;
+}
+
+int32_t pt_device_free(void* p) {
+    if (p) HIPCHK(hipFree(p));
+    return PT_OK;
+}
+
+int32_t pt_device_read(void* host_dst, const void* device_src, int64_t bytes) {
+    if (!host_dst || !device_src || bytes < 0) return fail(PT_E_INVALID, "pt_device_read: bad argument");
+    if (g.stream) HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemcpy(host_dst, device_src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
 int32_t pt_get_frame_stats(pt_frame_stats* out) {
     RC(need_init());
     if (!out) return fail(PT_E_INVALID, "NULL");

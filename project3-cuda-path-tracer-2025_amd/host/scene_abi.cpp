@@ -5,12 +5,9 @@
 #include <string>
 
 #include "scene.h"
+#include "scene_file.h"
 #include "png_decode.h"
 #include "image_io.h"
-
-struct pt_scene_file {
-    Scene* scene;
-};
 
 namespace {
 thread_local std::string g_scene_err;

@@ -92,6 +92,13 @@ ABI_SYMBOLS = [
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
     "pt_save_png", "pt_scene_load_ex", "pt_bvh_build", "pt_bvh_build_last_error", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
+    "pt_device_alloc", "pt_device_free", "pt_device_read",
+]
+# include/pt/pt_viewer.h (the headless interactive viewer)
+VIEWER_SYMBOLS = [
+    "pt_viewer_create", "pt_viewer_destroy", "pt_viewer_mouse_button", "pt_viewer_cursor_pos", "pt_viewer_key",
+    "pt_viewer_update_camera", "pt_viewer_run_frame", "pt_viewer_display", "pt_viewer_title", "pt_viewer_get_state",
+    "pt_viewer_save_image", "pt_viewer_last_error",
 ]
 
 
@@ -122,6 +129,14 @@ def _load():
         "pt_scene_load_ex": (i32, [ctypes.c_char_p, i32, i32, i32, i32, vp]),
         "pt_bvh_build": (i32, [vp, i32, vp, i32, vp, vp]),
         "pt_bvh_build_last_error": (ctypes.c_char_p, []),
+        "pt_device_alloc": (i32, [i64, vp]), "pt_device_free": (i32, [vp]), "pt_device_read": (i32, [vp, vp, i64]),
+        "pt_viewer_create": (i32, [vp, vp, ctypes.c_char_p, ctypes.c_char_p, vp]), "pt_viewer_destroy": (None, [vp]),
+        "pt_viewer_mouse_button": (i32, [vp, i32, i32, i32]),
+        "pt_viewer_cursor_pos": (i32, [vp, ctypes.c_double, ctypes.c_double]),
+        "pt_viewer_key": (i32, [vp, i32, i32, i32, i32]), "pt_viewer_update_camera": (i32, [vp, vp]),
+        "pt_viewer_run_frame": (i32, [vp, vp]), "pt_viewer_display": (i32, [vp, vp, i64]),
+        "pt_viewer_title": (i32, [vp, ctypes.c_char_p, i32]), "pt_viewer_get_state": (i32, [vp, vp]),
+        "pt_viewer_save_image": (i32, [vp, ctypes.c_char_p, i32]), "pt_viewer_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -388,6 +403,104 @@ class PathTracer:
         self._host_image = None
         if PathTracer._live is self:
             PathTracer._live = None
+
+
+class _ViewerState(ctypes.Structure):
+    _fields_ = [("zoom", ctypes.c_float), ("theta", ctypes.c_float), ("phi", ctypes.c_float),
+                ("iteration", ctypes.c_int32), ("camchanged", ctypes.c_int32), ("left", ctypes.c_int32),
+                ("right", ctypes.c_int32), ("middle", ctypes.c_int32), ("last_x", ctypes.c_double),
+                ("last_y", ctypes.c_double), ("should_close", ctypes.c_int32), ("exited", ctypes.c_int32),
+                ("traced_depth", ctypes.c_int32), ("saved_images", ctypes.c_int32),
+                ("og_look_at", ctypes.c_float * 3), ("camera", ctypes.c_uint8 * 92)]
+
+
+class Viewer:
+    """The reference's interactive viewer (main.cpp) without a window (include/pt/pt_viewer.h):
+    GLFW-style events in, runCuda() per display frame, the displayed pixels and saveImage out.
+    `scene` must be loaded with viewer_camera=False (the viewer applies main.cpp's recompute)."""
+
+    PRESS, RELEASE = 1, 0
+    LEFT, RIGHT, MIDDLE = 0, 1, 2
+    KEY_SPACE, KEY_S, KEY_ESCAPE = 32, 83, 256
+
+    def __init__(self, scene: SceneFile, image_dir: str = "../img", time_tag: str | None = None, **options):
+        self.scene = scene
+        self._opts = default_options(**options)
+        h = ctypes.c_void_p()
+        rc = lib.pt_viewer_create(scene._h, ctypes.byref(self._opts), image_dir.encode(),
+                                  None if time_tag is None else time_tag.encode(), ctypes.byref(h))
+        if rc != PT_OK:
+            raise PtError(f"pt_viewer_create: {lib.pt_viewer_last_error().decode(errors='replace')}")
+        self._h = h
+
+    def _c(self, rc, what):
+        if rc != PT_OK:
+            raise PtError(f"{what}: {lib.pt_viewer_last_error().decode(errors='replace')} (code {rc})")
+
+    def mouse_button(self, button: int, action: int, mods: int = 0):
+        self._c(lib.pt_viewer_mouse_button(self._h, button, action, mods), "mouse_button")
+
+    def cursor_pos(self, x: float, y: float):
+        self._c(lib.pt_viewer_cursor_pos(self._h, float(x), float(y)), "cursor_pos")
+
+    def key(self, key: int, action: int = 1):
+        self._c(lib.pt_viewer_key(self._h, key, 0, action, 0), "key")
+
+    def update_camera(self) -> bool:
+        r = ctypes.c_int32()
+        self._c(lib.pt_viewer_update_camera(self._h, ctypes.byref(r)), "update_camera")
+        return bool(r.value)
+
+    def run_frame(self) -> bool:
+        """One runCuda(); True when ITERATIONS were reached (image saved, tracer freed)."""
+        e = ctypes.c_int32()
+        self._c(lib.pt_viewer_run_frame(self._h, ctypes.byref(e)), "run_frame")
+        return bool(e.value)
+
+    def state(self) -> dict:
+        st = _ViewerState()
+        self._c(lib.pt_viewer_get_state(self._h, ctypes.byref(st)), "get_state")
+        d = {k: getattr(st, k) for k, _ in _ViewerState._fields_ if k not in ("og_look_at", "camera")}
+        d["og_look_at"] = np.array(st.og_look_at, np.float32)
+        d["camera"] = np.frombuffer(bytes(st.camera), CAMERA).copy()
+        return d
+
+    def title(self) -> str:
+        buf = ctypes.create_string_buffer(128)
+        self._c(lib.pt_viewer_title(self._h, buf, 128), "title")
+        return buf.value.decode()
+
+    def display(self) -> np.ndarray:
+        cam = self.state()["camera"]
+        w, h = int(cam["resolution"][0][0]), int(cam["resolution"][0][1])
+        out = np.empty((h, w, 3), np.uint8)
+        self._c(lib.pt_viewer_display(self._h, out.ctypes.data, out.size), "display")
+        return out
+
+    def save_image(self) -> str:
+        buf = ctypes.create_string_buffer(4096)
+        self._c(lib.pt_viewer_save_image(self._h, buf, 4096), "save_image")
+        return buf.value.decode()
+
+    def image(self) -> np.ndarray:
+        """The accumulated (not averaged) image of the frames since the last restart (the copy
+        pathtrace wrote into renderState->image), read from the tracer the viewer drives."""
+        cam = self.state()["camera"]
+        n = int(cam["resolution"][0][0]) * int(cam["resolution"][0][1])
+        out = np.empty((n, 3), np.float32)
+        _check(lib.pt_get_image(out.ctypes.data, out.size), "pt_get_image")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.pt_viewer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def rng_draws(seeds: np.ndarray, n: int) -> np.ndarray:
