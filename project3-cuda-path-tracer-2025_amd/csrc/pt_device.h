@@ -179,13 +179,13 @@ struct DevNode {
 // them.  ref >= 0 names the child's own pair record when ref < num_pairs, else the leaf
 // ref - num_pairs, whose triangles sit in the 4-slot group hot4[4 * leaf ..]; leaves are numbered
 // in the reference's visit order (push left, push right, pop: right subtree first), so a smaller
-// hot4 index is an earlier triangle in the reference's DFS.  s = max triangle edge below the
-// child (x 1.01), the size term of the certified t-cull.
+// hot4 index is an earlier triangle in the reference's DFS.  The cull constants are those of
+// cull_threshold for s = max triangle edge below the child (x 1.01), precomputed per child.
 struct DevPair {
     float4 l_lo;   // left box min.xyz  | left ref (int bits)
-    float4 l_hi;   // left box max.xyz  | left s
+    float4 l_hi;   // left box max.xyz  | left cull constants (A | d, 16 bits each, pack_cull)
     float4 r_lo;   // right box min.xyz | right ref (int bits)
-    float4 r_hi;   // right box max.xyz | right s
+    float4 r_hi;   // right box max.xyz | right cull constants
 };
 
 // VAR_BVH_QUAD: a 4-wide node collapsed from the reference's binary tree -- the up-to-4

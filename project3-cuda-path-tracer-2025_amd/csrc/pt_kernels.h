@@ -395,6 +395,17 @@ PT_DEV float cull_threshold(const SceneDev& sc, float entry, float s) {
     return T > 0.0f ? T : 0.0f;      // NaN (inf - inf on degenerate data) -> 0: never culled
 }
 PT_DEV uint32_t pack_ref(int ref, float T) { return ((uint32_t)ref << 16) | (__float_as_uint(T) >> 16); }
+// cull_threshold from the per-child constants the host packs into DevPair's hi.w (pack_cull in
+// pt_runtime.hip): high half A >= 1.002 c s + c E (1 + 1e-6), low half d >= 1 - (1 - 1e-6) /
+// (1 + 2c + 2e-6), both rounded UP to 16-bit floats.  T = (entry (1 - 2e-6) - A)(1 - d), two fmas
+// (each one rounding, covered by the 1e-6 factor), never exceeds the certified threshold
+// (entry (1 - 1e-6) - 1.001 c s - c E) / (1 + 2c + 1e-6).  NaN / negative -> 0: never culled.
+PT_DEV float cull_threshold_packed(float entry, float w) {
+    const uint32_t b = __float_as_uint(w);
+    const float A = __uint_as_float(b & 0xffff0000u), d = __uint_as_float(b << 16);
+    const float x = __builtin_fmaf(entry, 1.0f - 2e-6f, -A);
+    return __builtin_fmaxf(__builtin_fmaf(-d, x, x), 0.0f);
+}
 
 // traversal state of one ray on the pair layout
 struct TravState {
@@ -462,8 +473,8 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
         pl = aabb_decide(pr.l_lo, pr.l_hi, st.ro, st.rd, st.rr, st.exact, el);
         pb = aabb_decide(pr.r_lo, pr.r_hi, st.ro, st.rd, st.rr, st.exact, er);
     }
-    const float Tl = pl ? cull_threshold(sc, el, pr.l_hi.w) : 0.f;
-    const float Tr = pb ? cull_threshold(sc, er, pr.r_hi.w) : 0.f;
+    const float Tl = cull_threshold_packed(el, pr.l_hi.w);
+    const float Tr = cull_threshold_packed(er, pr.r_hi.w);
     pl = pl && !(t_best < Tl);
     pb = pb && !(t_best < Tr);
     const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);

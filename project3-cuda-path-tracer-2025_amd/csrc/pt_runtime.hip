@@ -1578,6 +1578,28 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             ok = ok && (int64_t)P + L <= 65535 && height + 1 <= MAXSTACK && !(o.variant & VAR_BVH_NODES);
             if (ok) {
                 auto ref = [&](int n) { return is_leaf[n] ? P + id[n] : id[n]; };
+                // cull_threshold_packed's constants for a child of cull size s (same c0 and E as
+                // SceneDev::cull_c0 / cull_E below), evaluated in double and rounded up
+                const float c0f = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
+                const float Ef = (float)(cull_extent * (1.0 + 1e-5));
+                auto pack_cull = [&](float sf) {
+                    auto up16 = [](double v) -> uint32_t {
+                        if (!(v >= 0.0)) v = HUGE_VAL;                  // NaN: never cull
+                        float f = (float)v;
+                        if ((double)f < v) f = std::nextafter(f, HUGE_VALF);
+                        uint32_t b;
+                        memcpy(&b, &f, 4);
+                        if (b & 0xffffu) b = (b & 0xffff0000u) + 0x10000u;   // up to 16 bits (inf stays inf)
+                        return b >> 16;
+                    };
+                    const double sd = sf, c = sd * sd * (double)c0f;
+                    const double A = c * sd * 1.002 + c * (double)Ef * (1.0 + 1e-6);
+                    const double d = 1.0 - (1.0 - 1e-6) / (1.0 + 2.0 * c + 2e-6);
+                    const uint32_t w = (up16(A) << 16) | up16(d);
+                    float f;
+                    memcpy(&f, &w, 4);
+                    return f;
+                };
                 pairs.resize(std::max(1, P));
                 for (int n = 0; n < nn; ++n) {
                     if (id[n] < 0 || is_leaf[n]) continue;
@@ -1592,7 +1614,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         float frf;
                         memcpy(&frf, &rf, 4);
                         *lo[k] = make_float4(nodes[c].lo.x, nodes[c].lo.y, nodes[c].lo.z, frf);
-                        *hi[k] = make_float4(nodes[c].hi.x, nodes[c].hi.y, nodes[c].hi.z, node_aux[c].y);
+                        *hi[k] = make_float4(nodes[c].hi.x, nodes[c].hi.y, nodes[c].hi.z, pack_cull(node_aux[c].y));
                     }
                 }
                 hot4.assign(4 * (size_t)L, DevTriHot{});
