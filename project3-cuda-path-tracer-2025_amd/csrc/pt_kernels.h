@@ -1004,14 +1004,20 @@ PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3
                                              __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
             const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
                                              __builtin_fmaxf(a2, b2));
-            const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
-            const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
-            // bitwise, not short-circuit: the compiler would otherwise branch around the away row
-            const uint32_t away = ((uint32_t)(qo > 0.5f) & (uint32_t)(u > 0.0f)) |
-                                  ((uint32_t)(qo < -0.5f) & (uint32_t)(u < 0.0f));
-            const uint32_t drop = away & (uint32_t)bounded & (uint32_t)(__float_as_int(C.z) != 0);
-            const uint32_t keep = (uint32_t)(t1 >= t0) & (drop ^ 1u) & (uint32_t)(i0 + k < ng);
-            bits |= keep << k;
+            const uint32_t slab = (uint32_t)(t1 >= t0) & (uint32_t)(i0 + k < ng);
+            const uint32_t row = (uint32_t)(__float_as_int(C.z) != 0);
+            uint32_t drop = 0;
+            // the away row only where some lane of the wave keeps this cube (wave-uniform branch):
+            // scenes with many geoms skip it for most of them
+            if (__any(slab & row)) {
+                const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
+                const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
+                // bitwise, not short-circuit: the compiler would otherwise branch around the row
+                const uint32_t away = ((uint32_t)(qo > 0.5f) & (uint32_t)(u > 0.0f)) |
+                                      ((uint32_t)(qo < -0.5f) & (uint32_t)(u < 0.0f));
+                drop = away & (uint32_t)bounded & row;
+            }
+            bits |= (slab & (drop ^ 1u)) << k;
         }
         cand |= (uint64_t)bits << i0;
     }
