@@ -301,7 +301,8 @@ def sub_config(ptamd, cfg):
            "value": round(st["segments_total"] / el / 1e6, 2), "unit": "Mpaths/s",
            "segments_per_frame": round(st["segments_total"] / steps, 1), "frames_per_pass": st["frames_per_pass"],
            "data": "synthetic stand-in meshes (reference OBJs absent)" if "obj" in scene_name else "reference scene",
-           "roofline": roofline(prof, st_prof, pipeline, steps, d, False),
+           "roofline": roofline(prof, st_prof, pipeline, steps, d, False,
+                                traffic_file="c4_bunny" if "bnnuy" in scene_name and res is None else None),
            "kernels": kernels_digest(prof, None)}
     if tag == "configs[4]":
         out["note"] = "BASELINE names 8 GPUs for this config; this sub-record is one GPU (bench.py --gpus 8 --scene ...)"
@@ -359,7 +360,7 @@ def _device_tensor(torch, ptr, n, device):
     return torch.as_tensor(_Cai(), device=f"cuda:{device}")
 
 
-def roofline(prof, st, pipeline, steps, depth, headline=True):
+def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None):
     """Dominant kernel, per launch.  Fused: the bounce kernel (camera|intersect|shade|gather|
     compact; `depth` launches per pass of F frames): algorithmic bytes = 48 B per path read
     (bounce > 0) + 48 B per survivor written + 24 B image read-modify-write (or 12 B plane store)
@@ -390,6 +391,12 @@ def roofline(prof, st, pipeline, steps, depth, headline=True):
     # measured HBM bytes per launch: the PMC run's bytes per frame x this run's frames per launch
     traffic = (int(pmc["hbm_bytes_per_frame"] * steps / launches) if pmc.get("hbm_bytes_per_frame")
                else pmc.get("hbm_bytes_per_launch"))
+    if traffic_file:
+        # a config with its own committed PMC digest (profiles/rNN_traffic_<tag>.json): both
+        # kernels of a bounce, bytes per frame scaled to this run's frames per launch pair
+        per_frame = sum(v.get("hbm_bytes_per_frame", 0) for k, v in _pmc_digest(traffic_file).items()
+                        if k in ("k_bounce", "k_bvh_bounce"))
+        traffic = int(per_frame * steps / launches) if per_frame else None
     line = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
@@ -411,6 +418,16 @@ def _pmc_file():
     d = os.path.join(REPO, "profiles")
     names = sorted(f for f in os.listdir(d) if f.endswith("_traffic.json") and f[1:3].isdigit()) if os.path.isdir(d) else []
     return names[-1] if names else "r01_traffic.json"
+
+
+def _pmc_digest(tag):
+    """The newest committed PMC digest of a config run, profiles/rNN_traffic_<tag>.json."""
+    d = os.path.join(REPO, "profiles")
+    names = sorted(f for f in os.listdir(d) if f.endswith(f"_traffic_{tag}.json")) if os.path.isdir(d) else []
+    if not names:
+        return {}
+    with open(os.path.join(d, names[-1])) as f:
+        return json.load(f)
 
 
 def _pmc(name):
@@ -455,7 +472,13 @@ def cpu_baseline(budget_s):
     v1, f1, e1 = run(1, budget_s)
     nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
     vn, fn, en = run(nt, budget_s / 2)
-    return {"value": round(v1, 3), "unit": "Mpaths/s", "cores": 1, "kind": "port",
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": round(v1, 3), "unit": "Mpaths/s", "cores": 1, "kind": "port", "cpu_model": model,
             "sample": f"cornell.json 400x400 depth 4 (BASELINE configs[0]), {f1} frames in {e1:.1f} s, "
                       f"{e1 / f1 * 1e3:.1f} ms/frame, oracle/pt_oracle.c single thread",
             "ms_per_frame": round(e1 / f1 * 1e3, 2),
