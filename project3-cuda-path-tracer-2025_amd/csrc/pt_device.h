@@ -14,6 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "pt/pt_libm.h"
@@ -112,19 +113,33 @@ PT_DEV f3 xform(const float* m, f3 v, float w) {
 // 192-byte geom: inverseTransform | transform | invTranspose (affine rows), a conservative
 // world-space box (center, half extents incl. a safety margin) used only to SKIP exact tests
 // that cannot change the result, + type + material
-struct DevGeom {
+// The first 112 bytes are what the exact tests read (DevGeomHot): the fused kernel stages only
+// that prefix in LDS, so a 44-geom table takes 4.9 KB instead of 8.4 KB of the block's LDS.
+struct DevGeomHot {
     float inv[12];
     float fwd[12];
-    float itr[12];
-    float box_lo[3];    // conservative world box (outward-rounded, margin included)
-    float box_hi[3];
     int32_t type;
     int32_t materialid;
     int32_t away_axis;  // cubes: object axis of the smallest scale for the pre-test's "away" drop
                         // (see away_on_axis); -1: none (spheres, or matrices too large to bound)
-    int32_t _pad[3];
+    int32_t _pad0;
+};
+static_assert(sizeof(DevGeomHot) == 112, "DevGeomHot");
+struct DevGeom {
+    float inv[12];
+    float fwd[12];
+    int32_t type;
+    int32_t materialid;
+    int32_t away_axis;
+    int32_t _pad0;
+    float itr[12];
+    float box_lo[3];    // conservative world box (outward-rounded, margin included)
+    float box_hi[3];
+    int32_t _pad[2];
 };
 static_assert(sizeof(DevGeom) == 192, "DevGeom");
+static_assert(offsetof(DevGeom, itr) == sizeof(DevGeomHot), "DevGeomHot is DevGeom's prefix");
+PT_DEV const DevGeomHot& hot(const DevGeom& g) { return *reinterpret_cast<const DevGeomHot*>(&g); }
 
 
 // Per-geom record of the candidate pre-test (block_intersect / wave_intersect), 48 bytes read
@@ -145,7 +160,7 @@ static_assert(sizeof(DevCull) == 48, "DevCull");
 // (m[9 + a] * 0 = +-0) is left out: it cannot change a nonzero u[a], and `u > 0` / `u < 0` are
 // false for either zero.  geom_test also requires dot(u, u) < inf; the caller guarantees it
 // (|rd| components <= 1e3 and |inv| entries <= 1e12, checked on the host).
-PT_DEV bool away_on_axis(const DevGeom& g, int a, f3 ro, f3 rd) {
+PT_DEV bool away_on_axis(const DevGeomHot& g, int a, f3 ro, f3 rd) {
     const float* m = g.inv;
     const float qo = (m[a] * ro.x + m[3 + a] * ro.y) + (m[6 + a] * ro.z + m[9 + a] * 1.0f);
     const float u = (m[a] * rd.x + m[3 + a] * rd.y) + m[6 + a] * rd.z;
@@ -259,7 +274,7 @@ PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normaliz
 // Every float operation and its order is the reference's.  Returns t (-1 on miss); `seed`
 // receives what the winner's normal is derived from: the box's object-space face normal
 // (tmin_n), or the sphere's object-space hit point.
-PT_DEV float geom_test(const DevGeom& g, f3 ro, f3 rd, f3& seed) {
+PT_DEV float geom_test(const DevGeomHot& g, f3 ro, f3 rd, f3& seed) {
     const f3 qo = xform(g.inv, ro, 1.0f);
     const f3 u = xform(g.inv, rd, 0.0f);
     const float uu = dot(u, u);

@@ -720,7 +720,7 @@ PT_DEV bool cull_geom(const DevGeom& g, const CullRay& c, float t_min) {
 // miss / facing conventions of pathtrace.cu:397-446
 // the winner's hit record from the primitive winner (t_min, win, seed) and the mesh result
 // (tb, u, v, slot of the winning triangle in `hot`; tb <= 0: none), pathtrace.cu:397-446
-PT_DEV Hit make_hit(const SceneDev& sc, const DevGeom* geoms, f3 rd, float t_min, int win, f3 seed, float tb, float u,
+PT_DEV Hit make_hit(const SceneDev& sc, f3 rd, float t_min, int win, f3 seed, float tb, float u,
                     float v, int tri, const DevTriHot* hot) {
     Hit h;
     h.tri = -1;
@@ -730,7 +730,7 @@ PT_DEV Hit make_hit(const SceneDev& sc, const DevGeom* geoms, f3 rd, float t_min
     int hit_index = -1;   // reference hit_geom_index: prim -> its materialid, mesh -> -2
     int mat = 0;
     if (win >= 0) {
-        const DevGeom& g = geoms[win];
+        const DevGeom& g = sc.geoms[win];   // itr: global (not in the LDS hot table)
         normal = normalize(xform(g.itr, seed, 0.0f));
         hit_index = g.materialid;
         mat = g.materialid;
@@ -774,7 +774,7 @@ PT_DEV Hit make_hit(const SceneDev& sc, const DevGeom* geoms, f3 rd, float t_min
 // winner normal, BVH meshes (bvhMeshIntersectionTest, strict `<` so primitives win ties),
 // miss / facing conventions of pathtrace.cu:397-446
 template <bool HAS_BVH, bool BVH_FAST = false, bool COUNT = false>
-PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, int* stack, float t_min, int win,
+PT_DEV Hit finish_hit(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_min, int win,
                       f3 seed, bool traverse = true) {
     float tb = -1.f, u = 0.f, v = 0.f;
     int tri = -1;
@@ -783,7 +783,7 @@ PT_DEV Hit finish_hit(const SceneDev& sc, const DevGeom* geoms, f3 ro, f3 rd, in
         tb = pairs ? bvh_intersect_pairs<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
            : BVH_FAST ? bvh_intersect_fast<COUNT>(sc, ro, rd, stack, t_min, u, v, tri)
                       : bvh_intersect<COUNT>(sc, ro, rd, stack, u, v, tri);
-    return make_hit(sc, geoms, rd, t_min, win, seed, tb, u, v, tri, pairs ? sc.hot4 : sc.hot);
+    return make_hit(sc, rd, t_min, win, seed, tb, u, v, tri, pairs ? sc.hot4 : sc.hot);
 }
 
 // computeIntersections for one ray (pathtrace.cu:298-448).  Per-geom work keeps only what
@@ -799,14 +799,14 @@ PT_DEV Hit intersect_scene(const SceneDev& sc, f3 ro, f3 rd, int* stack) {
         const DevGeom& g = sc.geoms[i];
         if (cull_geom(g, cr, t_min)) continue;
         f3 s;
-        float t = geom_test(g, ro, rd, s);
+        float t = geom_test(hot(g), ro, rd, s);
         if (t > 0.0f && t_min > t) {
             t_min = t;
             win = i;
             seed = s;
         }
     }
-    return finish_hit<HAS_BVH, BVH_FAST>(sc, sc.geoms, ro, rd, stack, t_min, win, seed);
+    return finish_hit<HAS_BVH, BVH_FAST>(sc, ro, rd, stack, t_min, win, seed);
 }
 
 // computeIntersections with the exact per-geom tests driven by a per-lane candidate queue:
@@ -830,7 +830,7 @@ PT_DEV float cull_entry(const DevGeom& g, const CullRay& c) {   // +inf: certain
     return (t1 >= t0) ? t0 : __builtin_inff();
 }
 template <bool TIMING = false, bool NEAR_FIRST = false>
-PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, float& t_min, int& win,
+PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeomHot* lgeoms, f3 ro, f3 rd, float& t_min, int& win,
                              f3& seed) {
     uint64_t tc0 = TIMING ? sec_clock() : 0;
     const CullRay cr = cull_ray(ro, rd);
@@ -866,10 +866,9 @@ PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
             if (cand != 0) {
                 const int i = __builtin_ctzll(cand);
                 cand &= cand - 1;
-                const DevGeom& g = lgeoms[i];
-                if (!cull_geom(g, cr, t_min)) {
+                if (!cull_geom(sc.geoms[i], cr, t_min)) {
                     f3 s;
-                    const float t = geom_test(g, ro, rd, s);
+                    const float t = geom_test(lgeoms[i], ro, rd, s);
                     if (t > 0.0f && (t < t_min || (t == t_min && win >= 0 && i < win))) {
                         t_min = t;
                         win = i;
@@ -895,11 +894,10 @@ PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
         if (cand != 0) {
             const int i = __builtin_ctzll(cand);
             cand &= cand - 1;
-            const DevGeom& g = lgeoms[i];
-            if (!cull_geom(g, cr, t_min)) {
+            if (!cull_geom(sc.geoms[i], cr, t_min)) {
                 f3 s;
                 if (TIMING) n_exact++;
-                float t = geom_test(g, ro, rd, s);
+                float t = geom_test(lgeoms[i], ro, rd, s);
                 if (t > 0.0f && t_min > t) {
                     t_min = t;
                     win = i;
@@ -915,18 +913,18 @@ PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f
     }
 }
 template <bool HAS_BVH, bool TIMING = false, bool BVH_FAST = false, bool NEAR_FIRST = false>
-PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeom* lgeoms, f3 ro, f3 rd, int* stack) {
+PT_DEV Hit intersect_scene_q(const SceneDev& sc, const DevGeomHot* lgeoms, f3 ro, f3 rd, int* stack) {
     float t_min;
     int win;
     f3 seed;
     prim_intersect_q<TIMING, NEAR_FIRST && !TIMING>(sc, lgeoms, ro, rd, t_min, win, seed);
     if (TIMING) {
         const uint64_t tc2 = sec_clock();
-        Hit h = finish_hit<HAS_BVH, BVH_FAST, true>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
+        Hit h = finish_hit<HAS_BVH, BVH_FAST, true>(sc, ro, rd, stack, t_min, win, seed);
         sec_add(SEC_FINISH, sec_clock() - tc2);
         return h;
     }
-    return finish_hit<HAS_BVH, BVH_FAST>(sc, lgeoms, ro, rd, stack, t_min, win, seed);
+    return finish_hit<HAS_BVH, BVH_FAST>(sc, ro, rd, stack, t_min, win, seed);
 }
 
 // surface attributes of the winner that shading reads only for textured / bump-mapped
@@ -971,7 +969,7 @@ PT_DEV void tex_fetch(const SceneDev& sc, int id, float x, float y, float out[4]
 // the sphere, whose exact test can round to a self-hit at t ~ 1e-4 (t1 = -b + sqrt(b^2 - ~0) =
 // 0), so only the reference arithmetic can reject them (a bounding-ball line test dropped 3 % of
 // all pairs and bought nothing).
-PT_DEV bool certain_exact_miss(const DevGeom& g, f3 ro, f3 rd, bool bounded) {
+PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) {
     const int a = g.away_axis;
     return g.type == PT_CUBE && (unsigned)a < 3u && bounded && away_on_axis(g, a, ro, rd);
 }
@@ -1031,7 +1029,7 @@ struct WaveLds {
     uint16_t task[WCAP];
 };
 template <bool COUNT = false>
-PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, WaveLds* W,
+PT_DEV void wave_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, f3 ro, f3 rd, WaveLds* W,
                            float& t_min, int& win, f3& seed) {
     const int lane = threadIdx.x & 63;
     uint64_t cand = 0;
@@ -1070,10 +1068,9 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
             if (cand != 0) {
                 const int i = __builtin_ctzll(cand);
                 cand &= cand - 1;
-                const DevGeom& g = lg[i];
-                if (!cull_geom(g, cr, t_min)) {
+                if (!cull_geom(sc.geoms[i], cr, t_min)) {
                     f3 s;
-                    const float t = geom_test(g, ro, rd, s);
+                    const float t = geom_test(lg[i], ro, rd, s);
                     if (t > 0.0f && t_min > t) {
                         t_min = t;
                         win = i;
@@ -1127,6 +1124,8 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 
 // of ceil(wave pairs / 64) (cornell: 79 pairs per wave on average -> 1.67 rounds each).  Same
 // per-lane scan of its own results afterwards, so the winner is unchanged.  Every thread of the
 // block must call it.
+// 768 pairs (3 per lane; cornell averages 1.2).  640 would fit one more 44-geom block per CU:
+// khaslana -0.7 %, cornell +0.8 % (A/B), so the headline keeps 768
 constexpr int BCAP = 4 * WCAP;
 struct BlockLds {
     float ro[3][BLOCK], rd[3][BLOCK];
@@ -1135,7 +1134,7 @@ struct BlockLds {
     int wsum[BLOCK / 64];
 };
 template <bool TIMING = false>
-PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3 ro, f3 rd, BlockLds* B,
+PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, f3 ro, f3 rd, BlockLds* B,
                             float& t_min, int& win, f3& seed) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t tc0 = TIMING ? sec_clock() : 0;
@@ -1178,10 +1177,9 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeom* lg, bool live, f3
             if (cand != 0) {
                 const int i = __builtin_ctzll(cand);
                 cand &= cand - 1;
-                const DevGeom& g = lg[i];
-                if (!cull_geom(g, cr, t_min)) {
+                if (!cull_geom(sc.geoms[i], cr, t_min)) {
                     f3 s;
-                    const float t = geom_test(g, ro, rd, s);
+                    const float t = geom_test(lg[i], ro, rd, s);
                     if (t > 0.0f && t_min > t) {
                         t_min = t;
                         win = i;

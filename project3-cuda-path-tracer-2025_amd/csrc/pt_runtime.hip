@@ -179,13 +179,14 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
     const bool lds_geoms = (QUEUE || REDIST) && sc.num_geoms <= LDS_GEOMS;
-    DevGeom* s_geoms = reinterpret_cast<DevGeom*>(s_dyn);
-    int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? sc.num_geoms * (int)(sizeof(DevGeom) / 16) : 0));
+    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
+    DevGeomHot* s_geoms = reinterpret_cast<DevGeomHot*>(s_dyn);
+    int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? sc.num_geoms * HOT4 : 0));
     WaveLds* s_wave_isect =
         reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH && !SPLIT ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
     if (lds_geoms) {   // per-lane candidate tests then read their geom from LDS, not L2
         const float4* src = reinterpret_cast<const float4*>(sc.geoms);
-        for (int k = tid; k < sc.num_geoms * (int)(sizeof(DevGeom) / 16); k += BLOCK) s_dyn[k] = src[k];
+        for (int k = tid; k < sc.num_geoms * HOT4; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
         __syncthreads();
     }
     const int gid = block_start + tid;
@@ -250,9 +251,9 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     if (live) {
         if (SPLIT) {
             queued = bvh_root_needed(sc, p.o, p.d, qt);
-            if (!queued) h = finish_hit<false>(sc, s_geoms, p.o, p.d, s_stack + tid, qt, qw, qs);
+            if (!queued) h = finish_hit<false>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else if (REDIST && lds_geoms) {
-            h = finish_hit<HAS_BVH, BVH_FAST>(sc, s_geoms, p.o, p.d, s_stack + tid, qt, qw, qs);
+            h = finish_hit<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else {
             h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST, FIRST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(BLOCK, 7) void k_bvh_bounce(SceneDev sc, QueueBuf q
         const int cw = __float_as_int(c.w);
         p.slot = cw & 255;
         const int win = (cw >> 8) - 1;
-        const Hit h = make_hit(sc, sc.geoms, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
+        const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
         shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     const bool surv = active && p.rb > 0;
@@ -844,7 +845,7 @@ template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
     const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && g.sc.num_geoms <= LDS_GEOMS;
-    const size_t geom_lds = lds ? sizeof(DevGeom) * g.sc.num_geoms : 0;
+    const size_t geom_lds = lds ? sizeof(DevGeomHot) * g.sc.num_geoms : 0;
     const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds
                                   ? std::max(sizeof(WaveLds) * (BLOCK / 64), (VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : 0)
                                   : 0;
