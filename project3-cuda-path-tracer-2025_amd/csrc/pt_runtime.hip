@@ -793,6 +793,19 @@ struct State {
 };
 State g;
 
+// Host <-> device copies and memsets of the runtime, ordered on the library's stream and
+// completed before returning.  g.stream is a non-blocking stream: the legacy null stream that
+// plain hipMemset / hipMemcpy use does not order against it, so a memset of FrameCtl could land
+// after a kernel enqueued behind it on g.stream (pt_test_camera saw a zeroed path count).
+hipError_t smemset(void* p, int v, size_t n) {
+    hipError_t e = hipMemsetAsync(p, v, n, g.stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(g.stream);
+}
+hipError_t smemcpy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, n, kind, g.stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(g.stream);
+}
+
 PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path[i][2]}; }
 
 // pt_profile_frames: every kernel of the frame is launched with hipExtLaunchKernel's start/stop
@@ -1094,7 +1107,7 @@ void free_all() {
 
 template <class T>
 int upload(T* d, const T* h, size_t n) {
-    if (n) HIPCHK(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    if (n) HIPCHK(smemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
     return PT_OK;
 }
 
@@ -1143,21 +1156,21 @@ void soa_to_paths(const std::vector<float4>& A, const std::vector<float4>& B, co
 int upload_paths(int buf, const pt_path_segment* paths, int64_t n) {
     std::vector<float4> A, B, C;
     paths_to_soa(paths, n, A, B, C);
-    HIPCHK(hipMemcpy(g.d_path[buf][0], A.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(g.d_path[buf][1], B.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(g.d_path[buf][2], C.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_path[buf][0], A.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_path[buf][1], B.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_path[buf][2], C.data(), n * sizeof(float4), hipMemcpyHostToDevice));
     return PT_OK;
 }
 int download_paths(int buf, int64_t n, pt_path_segment* out) {
     std::vector<float4> A(n), B(n), C(n);
-    HIPCHK(hipMemcpy(A.data(), g.d_path[buf][0], n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(B.data(), g.d_path[buf][1], n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(C.data(), g.d_path[buf][2], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(A.data(), g.d_path[buf][0], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(B.data(), g.d_path[buf][1], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(C.data(), g.d_path[buf][2], n * sizeof(float4), hipMemcpyDeviceToHost));
     soa_to_paths(A, B, C, n, out);
     return PT_OK;
 }
 int set_count(int slot, int value) {
-    HIPCHK(hipMemcpy(&g.d_ctl->cnt[slot][0][0], &value, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(&g.d_ctl->cnt[slot][0][0], &value, sizeof(int), hipMemcpyHostToDevice));
     return PT_OK;
 }
 
@@ -1786,7 +1799,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         RC(dalloc(&g.d_texinfo, info.size()));
         for (int i = 0; i < s->num_textures; ++i) {
             const pt_texture& t = s->textures[i];
-            HIPCHK(hipMemcpy(g.d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
+            HIPCHK(smemcpy(g.d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
         }
         RC(upload(g.d_texinfo, info.data(), info.size()));
         RC(dalloc(&g.d_hit_uvd0, (size_t)g.capacity));
@@ -1801,9 +1814,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     RC(dalloc(&g.d_tile_off, (size_t)ntiles));
     RC(dalloc(&g.d_image, (size_t)g.pixels_total * 3));
     if (g.batch > 1) RC(dalloc(&g.d_contrib, (size_t)g.pixels_total * 3 * g.batch));
-    HIPCHK(hipMemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
+    HIPCHK(smemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
     RC(dalloc(&g.d_ctl, 1));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     g.key_bits = 1;
     while ((1 << g.key_bits) < std::max(2, s->num_materials)) g.key_bits++;
 
@@ -1892,7 +1905,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         int depth = std::max(1, g.sc.trace_depth);
         if (g.opts.stream_compaction) {
             std::vector<int> cnt((size_t)depth * NSEG * CNT_PAD);
-            HIPCHK(hipMemcpy(cnt.data(), &g.d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+            HIPCHK(smemcpy(cnt.data(), &g.d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
             for (int k = 1; k < depth; ++k) {
                 int64_t live = 0;
                 for (int q = 0; q < NSEG; ++q) live += cnt[((size_t)k * NSEG + q) * CNT_PAD];
@@ -1942,7 +1955,7 @@ int32_t pt_get_image(float* host_out, int64_t n_floats) {
     RC(need_init());
     if (!host_out || n_floats < (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image buffer too small");
     HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(hipMemcpy(host_out, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(host_out, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total, hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
@@ -1958,7 +1971,7 @@ int32_t pt_set_image(const float* host_in, int64_t n_floats) {
     RC(need_init());
     if (!host_in || n_floats != (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
     HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(hipMemcpy(g.d_image, host_in, sizeof(float) * (size_t)n_floats, hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_image, host_in, sizeof(float) * (size_t)n_floats, hipMemcpyHostToDevice));
     return PT_OK;
 }
 
@@ -1980,7 +1993,7 @@ int32_t pt_device_free(void* p) {
 int32_t pt_device_read(void* host_dst, const void* device_src, int64_t bytes) {
     if (!host_dst || !device_src || bytes < 0) return fail(PT_E_INVALID, "pt_device_read: bad argument");
     if (g.stream) HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(hipMemcpy(host_dst, device_src, (size_t)bytes, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(host_dst, device_src, (size_t)bytes, hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
@@ -1989,7 +2002,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
     if (!out) return fail(PT_E_INVALID, "NULL");
     HIPCHK(hipStreamSynchronize(g.stream));
     FrameCtl ctl;
-    HIPCHK(hipMemcpy(&ctl, g.d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(&ctl, g.d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof(*out));
     out->iteration = ctl.iter;
     out->bounces = std::max(1, g.sc.trace_depth);
@@ -2019,7 +2032,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
 int32_t pt_reset_stats(void) {
     RC(need_init());
     HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2029,14 +2042,14 @@ int32_t pt_reset_stats(void) {
 int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(need_init());
     if (!out || n < g.local_pixels) return fail(PT_E_INVALID, "output too small");
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels, 1);
     hipLaunchKernelGGL(k_camera, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g.stream));
     release_graph();
     RC(download_paths(0, g.local_pixels, out));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2069,14 +2082,14 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
     HIPCHK(hipStreamSynchronize(g.stream));
     std::vector<float4> nt(n);
     std::vector<int> mat(n);
-    HIPCHK(hipMemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
     std::vector<float4> a0, a1;
     if (uvd0) {
         a0.resize(n);
         a1.resize(n);
-        HIPCHK(hipMemcpy(a0.data(), uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(a1.data(), uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(smemcpy(a0.data(), uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
+        HIPCHK(smemcpy(a1.data(), uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
     }
     if (tmp_attr) {
         (void)hipFree(uvd0);
@@ -2094,7 +2107,7 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
         }
     }
     release_graph();
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2113,8 +2126,8 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
         if (isects[i].t > 0.0f && (mat[i] < 0 || mat[i] >= std::max(1, g.sc.num_mats)))
             return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
     }
-    HIPCHK(hipMemcpy(g.d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
     if (g.d_hit_uvd0) {
         std::vector<float4> a0(n), a1(n);
         for (int64_t i = 0; i < n; ++i) {
@@ -2122,8 +2135,8 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
             a0[i] = make_float4(x.uv.x, x.uv.y, x.dpdu.x, x.dpdu.y);
             a1[i] = make_float4(x.dpdu.z, x.dpdv.x, x.dpdv.y, x.dpdv.z);
         }
-        HIPCHK(hipMemcpy(g.d_hit_uvd0, a0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(g.d_hit_uvd1, a1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(smemcpy(g.d_hit_uvd0, a0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(smemcpy(g.d_hit_uvd1, a1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
     }
     HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
     hipLaunchKernelGGL(k_shade, dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), hits,
@@ -2133,7 +2146,7 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
     HIPCHK(hipStreamSynchronize(g.stream));
     release_graph();
     RC(download_paths(0, n, paths));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2143,8 +2156,8 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     RC(upload_paths(0, paths, n));
     std::vector<int> al(std::max<int64_t>(1, n));
     for (int64_t i = 0; i < n; ++i) al[i] = paths[i].remainingBounces > 0;   // PathAlive
-    if (n) HIPCHK(hipMemcpy(g.d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    if (n) HIPCHK(smemcpy(g.d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     RC(set_count(0, (int)n));
     if (n > 0) {   // the pipeline's launch sequence
         launch_compact<CITEMS>(pathbuf(0), pathbuf(1), staged_count(0), &g.d_ctl->cnt[1][0][0], (int)n);
@@ -2152,11 +2165,11 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     }
     HIPCHK(hipStreamSynchronize(g.stream));
     int na = 0;
-    HIPCHK(hipMemcpy(&na, &g.d_ctl->cnt[1][0][0], sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(&na, &g.d_ctl->cnt[1][0][0], sizeof(int), hipMemcpyDeviceToHost));
     if (alive_out) *alive_out = na;
     release_graph();
     RC(download_paths(1, na, out));
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2170,7 +2183,7 @@ int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm)
         mat[i] = isects[i].materialId;
         if (mat[i] < 0 || mat[i] >= nk) return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
     }
-    HIPCHK(hipMemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
     RC(set_count(0, (int)n));
     const int ntiles = (int)((n + STILE - 1) / STILE);
     hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
@@ -2180,9 +2193,9 @@ int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm)
                        g.key_bits, g.d_tile_hist, g.d_perm);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(hipMemcpy(perm, g.d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(perm, g.d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
     release_graph();
-    HIPCHK(hipMemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2194,10 +2207,10 @@ int32_t pt_test_rng(const int32_t* iid, int64_t m, int32_t n, float* out) {
     float* d_out = nullptr;
     HIPCHK(hipMalloc(&d_iid, sizeof(int) * 3 * m));
     HIPCHK(hipMalloc(&d_out, sizeof(float) * m * n));
-    HIPCHK(hipMemcpy(d_iid, iid, sizeof(int) * 3 * m, hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(d_iid, iid, sizeof(int) * 3 * m, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_rng, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, 0, d_iid, (int)m, n, d_out);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(out, d_out, sizeof(float) * m * n, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(out, d_out, sizeof(float) * m * n, hipMemcpyDeviceToHost));
     (void)hipFree(d_iid);
     (void)hipFree(d_out);
     return PT_OK;
@@ -2211,11 +2224,11 @@ int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4*
     pt_uchar4* d_pbo = nullptr;
     HIPCHK(hipMalloc(&d_img, sizeof(float) * 3 * n));
     HIPCHK(hipMalloc(&d_pbo, sizeof(pt_uchar4) * n));
-    HIPCHK(hipMemcpy(d_img, image, sizeof(float) * 3 * n, hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(d_img, image, sizeof(float) * 3 * n, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_to_pbo, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0, d_img, d_pbo, (int)n,
                        iteration);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpy(pbo, d_pbo, sizeof(pt_uchar4) * n, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(pbo, d_pbo, sizeof(pt_uchar4) * n, hipMemcpyDeviceToHost));
     (void)hipFree(d_img);
     (void)hipFree(d_pbo);
     return PT_OK;
@@ -2226,11 +2239,13 @@ int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset) {
     if (!out || n < 0 || n > 16) return fail(PT_E_INVALID, "bad arguments");
     HIPCHK(hipStreamSynchronize(g.stream));
     unsigned long long tmp[16];
-    HIPCHK(hipMemcpyFromSymbol(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyFromSymbolAsync(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost, g.stream));
+    HIPCHK(hipStreamSynchronize(g.stream));
     for (int i = 0; i < n; ++i) out[i] = tmp[i];
     if (reset) {
         memset(tmp, 0, sizeof tmp);
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_sections), tmp, sizeof tmp, 0, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sections), tmp, sizeof tmp, 0, hipMemcpyHostToDevice, g.stream));
+        HIPCHK(hipStreamSynchronize(g.stream));
     }
     return PT_OK;
 }
