@@ -15,11 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 TILE = 16
 # image -> (scene, samples).  README.md:112 "basic diffuse output" (cornell.json; 5000 spp, the
 # scene's ITERATIONS), README.md:267-270 "Transmissive material" (5000samp) and "Glass material"
-# (1809samp).  Two other candidates do not match any scene of the checkout and are left out:
+# (1809samp).  Candidates that match no scene of the checkout are left out (tools/ref_render_compare.py
+# measured them): the microfacet images (README.md:300-303; other light and parameters), the
+# aperture series (README.md:246; mean |tile difference| ~4.3),
 # REFERENCE_cornell.5000samp.png (the course's base-code image: mean 31.8 vs 38.6) and
 # cornell.2025-09-25_21-04-50z.5000samp.png (a transmissive bug image, README.md:326).
 CASES = {
     "diffuse.png": ("cornell.json", 5000),
+    # README.md:133-136: the render of the measurement that gives BASELINE's 42.204 ms/frame
+    "diffuse_stream_compaction.png": ("cornell.json", 5000),
     "cornell.2025-09-25_23-38-19z.5000samp.png": ("cornell_transmissive_test.json", 5000),
     "cornell.2025-09-25_23-49-57z.1809samp.png": ("cornell_glass_test.json", 1809),
 }
