@@ -51,6 +51,10 @@ def test_no_device_fails_loudly(ptamd):
     sc = ptamd.SceneFile(scene_path("cornell"), res=(16, 16))
     with pytest.raises(ptamd.PtError):
         ptamd.PathTracer(sc)
+    p = ctypes.c_void_p(1)
+    assert ptamd.lib.pt_device_alloc(1024, ctypes.byref(p)) == -4 and not p.value   # PT_E_NODEVICE
+    assert ptamd.lib.pt_device_alloc(0, ctypes.byref(p)) == -1                        # PT_E_INVALID
+    assert ptamd.lib.pt_device_free(None) == 0
 
 
 def test_scene_view_round_trip(ptamd):
