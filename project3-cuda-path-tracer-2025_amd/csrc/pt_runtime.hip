@@ -310,6 +310,75 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     if (TIMING && active) sec_add(SEC_STORE, sec_clock() - tc);
 }
 
+// Single-frame passes (the API's pathtrace(), F = 1): bounces `bounce` .. depth-1 of a
+// primitive-only scene in ONE launch.  Each block keeps its paths in registers and loops over the
+// remaining bounces (block-wide exact-test exchange, shading, gather at termination) until none of
+// its paths is alive, with no compaction in between: the late bounces of a lone frame are a few
+// thousand waves each, bound by launch and drain latency rather than by work.  Per-path
+// arithmetic, RNG keys and the gather are those of k_bounce, so the image is the same bit for
+// bit; per-bounce live counts go to the same counters (one atomic per block per bounce).
+template <int VAR>
+__global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCtl* ctl, float* __restrict__ image,
+                                               int bounce, int seg_stride, int depth) {
+    extern __shared__ float4 s_dyn[];
+    __shared__ int s_cnt[BLOCK / 64];
+    const int iter = ctl->iter;
+    const int batch = ctl->batch;
+    int segoff[NSEG + 1];
+    segoff[0] = 0;
+#pragma unroll
+    for (int s = 0; s < NSEG; ++s) segoff[s + 1] = segoff[s] + ctl->cnt[bounce][s][0];
+    const int n = segoff[NSEG];
+    const int block_start = blockIdx.x * BLOCK;
+    if (block_start >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
+    DevGeomHot* s_geoms = reinterpret_cast<DevGeomHot*>(s_dyn);
+    BlockLds* s_block = reinterpret_cast<BlockLds*>(s_dyn + sc.num_geoms * HOT4);
+    {
+        const float4* src = reinterpret_cast<const float4*>(sc.geoms);
+        for (int k = tid; k < sc.num_geoms * HOT4; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
+        __syncthreads();
+    }
+    const int gid = block_start + tid;
+    const bool active = gid < n;
+    PathReg p;
+    p.rb = 0;
+    if (active) {
+        int sl = 0;
+#pragma unroll
+        for (int k = 1; k < NSEG; ++k) sl += (gid >= segoff[k]) ? 1 : 0;
+        int sofs = 0;
+#pragma unroll
+        for (int k = 1; k < NSEG; ++k) sofs = (sl == k) ? segoff[k] : sofs;
+        p = load_path(in, sl * seg_stride + (gid - sofs));
+    }
+    const int seg = blockIdx.x & (NSEG - 1);
+    for (int b = bounce; b < depth; ++b) {
+        const bool live = active && p.rb > 0;
+        float qt = 0.f;
+        int qw = -1;
+        f3 qs = mk(0.f, 0.f, 0.f);
+        block_intersect<false>(sc, s_geoms, live, p.o, p.d, s_block, qt, qw, qs);
+        if (live) {
+            const Hit h = finish_hit<false>(sc, p.o, p.d, nullptr, qt, qw, qs);
+            shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+            if (p.rb <= 0) gather_into_image(image, sc, batch, p);
+        }
+        // paths entering bounce b + 1 (k_bounce's survivor count for this bounce)
+        const bool surv = live && p.rb > 0;
+        const uint64_t m = __ballot(surv);
+        if (lane == 0) s_cnt[tid >> 6] = __popcll(m);
+        __syncthreads();
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) tot += s_cnt[i];
+        if (tid == 0 && tot) atomicAdd(&ctl->cnt[b + 1][seg][0], tot);
+        __syncthreads();
+        if (tot == 0) break;          // block-uniform
+    }
+}
+
 // VAR_BVH_SPLIT, second half of a bounce: the queued paths, 64 to a wave, traverse the mesh
 // (bvh_intersect_pairs via finish_hit, entering with their primitive winner), are shaded, and
 // gathered / compacted into the same output segments as k_bounce (blockIdx % NSEG; the host
@@ -944,15 +1013,36 @@ void launch_compact(PathBuf pi, PathBuf po, const int* n_in, int* n_out, int npa
 
 // Enqueue one pass's kernels (everything after k_frame_begin) on g.stream: `batch` frames
 // traced together as one wavefront of local_pixels x batch paths.
+// single-frame passes of primitive-only scenes run bounces tail_from() .. depth-1 as one k_tail
+// launch (PT_TAIL=0 turns it off for A/B); 0: no tail launch
+int tail_from(int batch) {
+    static const bool off = getenv("PT_TAIL") && atoi(getenv("PT_TAIL")) == 0;
+    const int depth = g.sc.trace_depth;
+    const bool lds = g.sc.num_geoms <= LDS_GEOMS;
+    if (off || batch != 1 || g.has_bvh || !lds || depth < 3 ||
+        effective_variant(false, g.opts.variant, false) != (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
+        return 0;
+    static const int from = getenv("PT_TAIL_FROM") ? atoi(getenv("PT_TAIL_FROM")) : 0;   // tools: A/B
+    return std::min(depth - 1, std::max(1, from > 0 ? from : depth / 2));
+}
+
 int enqueue_pass_body(int batch) {
     const int depth = g.sc.trace_depth;
     const int npaths = g.local_pixels * batch;
     const int nb = nblocks(npaths);
     const int nbounces = std::max(1, depth);
     if (g.opts.pipeline == PT_PIPELINE_FUSED) {
-        for (int b = 0; b < nbounces; ++b) {
+        const int t = tail_from(batch);
+        for (int b = 0; b < (t ? t : nbounces); ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
             launch_bounce(b == 0, g.has_bvh, g.opts.variant & ~VAR_BVH_NODES, dim3(nb), in, out, b);
+            HIPCHK(hipGetLastError());
+        }
+        if (t) {
+            constexpr int V = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST;
+            const size_t lds = sizeof(DevGeomHot) * g.sc.num_geoms + sizeof(BlockLds);
+            launch(100 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
+                   g.seg_stride, depth);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
