@@ -1019,7 +1019,8 @@ int tail_from(int batch) {
     static const bool off = getenv("PT_TAIL") && atoi(getenv("PT_TAIL")) == 0;
     const int depth = g.sc.trace_depth;
     const bool lds = g.sc.num_geoms <= LDS_GEOMS;
-    if (off || batch != 1 || g.has_bvh || !lds || depth < 3 ||
+    static const bool any_batch = getenv("PT_TAIL_BATCH") && atoi(getenv("PT_TAIL_BATCH")) != 0;   // tools: A/B
+    if (off || (batch != 1 && !any_batch) || g.has_bvh || !lds || depth < 3 ||
         effective_variant(false, g.opts.variant, false) != (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
         return 0;
     static const int from = getenv("PT_TAIL_FROM") ? atoi(getenv("PT_TAIL_FROM")) : 0;   // tools: A/B
