@@ -981,7 +981,7 @@ PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) 
 // one scalar-memory round trip instead of two per geom.  The host pads the record array to a
 // multiple of 4; bits of pad records are masked off by the (wave-uniform) index test.
 #ifndef CULL_GROUP
-#define CULL_GROUP 2
+#define CULL_GROUP 4
 #endif
 PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
     const float4* rec = reinterpret_cast<const float4*>(sc.cull);
