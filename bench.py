@@ -55,7 +55,7 @@ SUB_CONFIGS = [
     ("configs[2]", "cornell_glass_test.json", None, None, True, "staged", 48, 4),
     ("configs[2] fused", "cornell_glass_test.json", None, None, False, "fused", 64, 8),
     ("configs[3]", "cornell_obj_bnnuy.json", None, None, False, "fused", 48, 4),
-    ("configs[4]", "cornell_obj_khaslana.json", (1600, 1600), 12, False, "fused", 16, 2),
+    ("configs[4]", "cornell_obj_khaslana.json", (1600, 1600), 12, False, "fused", 32, 2),
 ]
 
 

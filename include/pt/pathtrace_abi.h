@@ -87,7 +87,7 @@ typedef struct pt_options {
                                     results are bit-identical for every value.  Default
                                     2|8|16|32|128 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..256;
-                                    0 = auto: ~42M paths in flight, e.g. 64 at 800x800, 256 for
+                                    0 = auto: ~84M paths in flight, e.g. 128 at 800x800, 256 for
                                     a 1/8 pixel shard of it).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in
                                     per-frame planes that are added in frame order. */

@@ -801,13 +801,13 @@ int dalloc(T** p, size_t n) {
 }
 
 constexpr int MAXF = 256;                   // frames per pass, upper bound (slot: 8 bits of a queue entry)
-// auto F: up to ~42M paths at bounce 0 -> 800x800: F = 64, 1600x1600: F = 16.  A/B (ms/frame):
+// auto F: up to ~84M paths at bounce 0 -> 800x800: F = 128, 1600x1600: F = 32.  A/B (ms/frame):
 // cornell 800^2 F = 8 0.0992, 16 0.0949 (0.0937), 32 0.0921; bunny 800^2 F = 8 0.685, 16 0.633;
 // khaslana 1600^2 F = 2 2.52, 4 1.95 (1.93), 8 1.66 (earlier kernels: F = 1 0.214, 2 0.161,
 // 4 0.137, 8 0.129).  Round 2 (tools/autof_ab.sh, target 21M / 42M / 84M paths): khaslana
-// 1600^2 d12 1.38 / 1.27 / 1.23, bunny 0.397 / 0.388 / 0.391, cornell flat.  ~8 GB of path
-// buffers + 2.6 GB traversal queue at 1600^2, F = 16 (of 288 GB).
-constexpr int64_t AUTO_BATCH_PATHS = 42000000;
+// 1600^2 d12 1.38 / 1.27 / 1.23, bunny 0.397 / 0.388 / 0.391, cornell flat.  ~16 GB of path
+// buffers + 5.2 GB traversal queue at 1600^2, F = 32 (of 288 GB).
+constexpr int64_t AUTO_BATCH_PATHS = 84000000;
 
 struct State {
     bool inited = false;
@@ -1310,7 +1310,7 @@ int32_t pt_free(void) {
 }
 
 // frames per pass when pt_options.frames_per_pass == 0: enough paths in flight to fill the
-// chip in the late, mostly-terminated bounces (~42M paths at bounce 0), at most MAXF
+// chip in the late, mostly-terminated bounces (~84M paths at bounce 0), at most MAXF
 int auto_batch(int local_pixels) {
     static const int64_t target = getenv("PT_AUTO_PATHS") ? atoll(getenv("PT_AUTO_PATHS")) : AUTO_BATCH_PATHS;  // tools: A/B
     int f = 1;

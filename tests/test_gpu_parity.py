@@ -468,14 +468,14 @@ def test_intersections_match_reference(name, variant, ptamd):
 @pytest.mark.parametrize("name", ["cornell", "cornell_obj_bnnuy"])
 def test_benched_configuration_bitexact(name, oracle, ptamd):
     """Exactly what bench.py times for BASELINE configs[1] / configs[3]: 800x800, default options
-    (variant 186: block exchange, split BVH queue, pair layout), auto frames-per-pass (64 at 800x800:
+    (variant 186: block exchange, split BVH queue, pair layout), auto frames-per-pass (128 at 800x800:
     the 40 frames run as one wavefront pass of 40).  Image and per-bounce live totals == the oracle's
     (OpenMP over paths) frame by frame."""
     a, b = _oracle_pair(oracle, ptamd, name, None)
     tr = ptamd.PathTracer(b)
     tr.trace_frames(1, 40)
     st = tr.stats()
-    assert st["frames_per_pass"] == 64 and st["last_pass_frames"] == 40 and st["frames_total"] == 40
+    assert st["frames_per_pass"] == 128 and st["last_pass_frames"] == 40 and st["frames_total"] == 40
     r = oracle.Renderer(a, oracle.options(**BIT))
     tot = np.zeros(a.trace_depth, np.int64)
     for it in range(1, 41):
