@@ -16,7 +16,7 @@ st() {   # st TAG ARGS...
 }
 st fused --steps 100 --warmup 10
 st c4_bunny --steps 48 --warmup 8 --scene scenes/cornell_obj_bnnuy.json
-st c5_khaslana --steps 16 --warmup 4 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
+st c5_khaslana --steps 32 --warmup 4 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
 PMC_TAG=fused_ bash tools/pmc.sh || exit 4
 PMC_TAG=bvh2_ bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json || exit 5
 PMC_TAG=imta_ PMC_SETS="SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_SMEM,SQ_INSTS_VMEM,SQ_WAVE_CYCLES;SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE,TA_BUSY_avr,TA_TA_BUSY_sum" \
