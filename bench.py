@@ -181,6 +181,9 @@ def main():
     if world == 1:
         # kernel durations: the next K frames replayed eagerly with events around every kernel
         tr.reset_stats()
+        gap = float(os.environ.get("PT_BENCH_PROF_GAP", "0"))
+        if gap > 0:
+            time.sleep(gap)
         prof = tr.profile(it, args.steps)
         st_prof = tr.stats()
         spread = None if args.no_spread else pass_spread(tr, it + args.steps, st_prof["frames_per_pass"])
