@@ -48,6 +48,7 @@ REF_MS_PER_FRAME = 42.204      # reference README.md:136, RTX 3060 Laptop, compa
 STATE_BYTES = 48               # one path in flight: 3 x float4 (origin|pixel, dir|bounces, rgb|-)
 IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3 (1-frame pass)
 PLANE_STORE_BYTES = 12         # terminated path of an F-frame pass: float3 store to its frame's plane
+QUEUE_ENTRY_BYTES = 64         # mesh scenes: a ray queued for k_bvh_bounce (written by k_bounce, read back)
 N_CUS = 256                    # MI355X compute units
 
 # BASELINE.json configs[2..4] as sub-records of the N=1 line: (tag, scene, res, depth, sort, pipeline, steps, warmup)
@@ -337,7 +338,7 @@ def pass_spread(tr, first_iteration, frames_per_pass, passes=16):
 def api_frame_ms(tr, first_iteration, frames=40, warm=5):
     """API-faithful frame: pathtrace(pbo, 0, iter) as main.cpp:463 calls it -- one
     frame per call (F = 1), the accumulated image copied into host memory every call
-    (pathtrace.cu:783; the library page-locks the caller's buffer once) -- median / p90 of the
+    (pathtrace.cu:783; the caller's pageable buffer, as the reference's cudaMemcpy) -- median / p90 of the
     host wall time per call, with and without that copy."""
     def run(copy, first):
         ts = []
@@ -353,7 +354,7 @@ def api_frame_ms(tr, first_iteration, frames=40, warm=5):
     m_copy, p_copy = run(True, first_iteration)
     m_nc, p_nc = run(False, first_iteration + warm + frames)
     return {"ms_per_frame": m_copy, "p90": p_copy, "ms_per_frame_no_copy": m_nc, "p90_no_copy": p_nc,
-            "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into page-locked host memory per call"}
+            "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into the caller's pageable host memory per call"}
 
 
 def _device_tensor(torch, ptr, n, device):
@@ -367,10 +368,11 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
     """Dominant kernel, per launch.  Fused: the bounce kernel (camera|intersect|shade|gather|
     compact; `depth` launches per pass of F frames): algorithmic bytes = 48 B per path read
     (bounce > 0) + 48 B per survivor written + 24 B image read-modify-write (or 12 B plane store)
-    per terminated path.  Staged: the compaction scatter kernel: 4 B flag per path in + 96 B per
+    per terminated path, + (mesh scenes) the traversal queue's round trip per queued ray.  Staged: the compaction scatter kernel: 4 B flag per path in + 96 B per
     survivor (48 B read + 48 B written).  achieved = bytes per launch / average launch duration
     (hipExtLaunchKernel dispatch timestamps, pt_profile_frames)."""
     tot = st["live_total"]                 # per-bounce live counts summed over the timed frames
+    queued = st.get("queued_total") or [0] * len(tot)
     launches = depth * prof["passes"]
     nbytes = 0
     for b in range(depth):
@@ -378,6 +380,7 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
         if pipeline == "fused":
             gather = IMAGE_RMW_BYTES if st["frames_per_pass"] == 1 else PLANE_STORE_BYTES
             nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + gather * (n_in - n_out)
+            nbytes += 2 * QUEUE_ENTRY_BYTES * queued[b]      # traversal queue round trip
         else:
             nbytes += 4 * n_in + 2 * STATE_BYTES * n_out
     if pipeline == "fused" and any(prof["bvh_ms"][:depth]):
@@ -447,7 +450,7 @@ def _pmc(name):
 
 def pcie_copy_ms(tr):
     """The reference copies the accumulated image to the host every frame (pathtrace.cu:783):
-    time one such copy into fresh pageable memory (the `api` record uses page-locked memory)."""
+    time one such copy into fresh pageable memory (the `api` record copies into a reused buffer)."""
     tr.synchronize()
     t0 = time.perf_counter()
     for _ in range(5):

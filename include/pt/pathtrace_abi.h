@@ -104,6 +104,8 @@ typedef struct pt_frame_stats {
     int64_t segments_total;      /* path segments traced over those frames */
     int32_t frames_per_pass;     /* resolved F; live[] / segments above cover the last pass */
     int32_t last_pass_frames;
+    int64_t queued_total[65];    /* mesh scenes, fused pipeline: per-bounce paths queued for the BVH
+                                    traversal kernel, summed over frames_total frames (0 otherwise) */
 } pt_frame_stats;
 
 int32_t pt_abi_version(void);
@@ -125,10 +127,8 @@ int32_t pt_free(void);
  * 1-based `iteration`, add it into the accumulated image, write the 8-bit preview into
  * `pbo_device` (a DEVICE pointer of width*height pt_uchar4, or NULL), and copy the
  * accumulated (not averaged) image into `host_image` (width*height*3 floats, or NULL) —
- * the reference copies into scene->state.image every call (pathtrace.cu:783-784).  The library
- * page-locks `host_image` (hipHostRegister) on first use so the copy runs at PCIe rate; like
- * state.image it must stay the same live allocation across calls — passing a different pointer
- * re-registers, pt_free releases it. */
+ * the reference copies into scene->state.image every call (pathtrace.cu:783-784).  The copy goes
+ * straight into the caller's (pageable) memory; nothing about `host_image` is kept between calls. */
 int32_t pt_trace(pt_uchar4* pbo_device, int32_t frame, int32_t iteration, float* host_image);
 
 /* Trace `count` frames with iterations first_iteration .. first_iteration+count-1, image stays
@@ -231,6 +231,10 @@ typedef struct pt_kernel_times {
     int32_t passes;              /* wavefront passes the `frames` frames were traced in */
     float combine_ms;            /* k_combine (per-frame planes -> image) per frame */
     float bvh_ms[64];            /* split BVH traversal (variant 32): k_bvh_bounce's part of bounce_ms[b] */
+    float tail_ms;               /* single-frame passes of primitive-only scenes: the one k_tail launch that
+                                    runs bounces tail_from .. depth-1 (per pass; bounce_ms[b >= tail_from]
+                                    stay 0 then) */
+    int32_t tail_from;           /* first bounce k_tail ran (0: no k_tail launch) */
 } pt_kernel_times;
 /* Trace `count` frames with iterations first_iteration.. eagerly, every kernel launched with
  * hipExtLaunchKernel start/stop events (timestamps of that dispatch itself) and no host

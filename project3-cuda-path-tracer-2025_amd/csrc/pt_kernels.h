@@ -84,6 +84,7 @@ struct FrameCtl {
     int _pad[2];
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
+    unsigned long long qtot[MAXB + 1];      // the same for qcnt (paths of bounce b queued for traversal)
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
     int qcnt[MAXB + 1][CNT_PAD];            // VAR_BVH_SPLIT: paths of bounce b queued for traversal
 };

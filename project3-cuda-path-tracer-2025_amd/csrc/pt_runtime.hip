@@ -48,6 +48,7 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
             unsigned long long s = 0;
             for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k][0];
             ctl->tot[b] += s;
+            ctl->qtot[b] += (unsigned)ctl->qcnt[b][0];
         }
     }
     __syncthreads();
@@ -816,7 +817,12 @@ struct State {
     hipStream_t stream = nullptr;
     SceneDev sc{};
     int width = 0, height = 0, pixels_total = 0, local_pixels = 0;
+    // per-pass buffers are sized lazily (ensure_frames): a caller that only ever traces single
+    // frames (the drop-in pathtrace(), the viewer) holds one frame's worth, not a whole pass's
     int seg_stride = 0, capacity = 0;
+    int alloc_frames = 0;            // frames per pass the path buffers / queue / planes hold now
+    bool staged_alloc = false;       // hit / alive / permutation / tile buffers at `capacity`
+    int num_tex = 0;
     bool has_bvh = false;
     int stack_depth = 0;
     size_t bvh_lds = 0;
@@ -857,12 +863,9 @@ struct State {
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
     int key_bits = 1;
-    // pt_trace's host image (the reference's scene->state.image): page-locked with hipHostRegister
-    // on first use so the per-frame D->H copy (pathtrace.cu:783) runs at full PCIe rate
-    void* host_reg = nullptr;
-    size_t host_reg_bytes = 0;
 };
 State g;
+int ensure_frames(int frames);
 
 // Host <-> device copies and memsets of the runtime, ordered on the library's stream and
 // completed before returning.  g.stream is a non-blocking stream: the legacy null stream that
@@ -885,7 +888,7 @@ PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path
 struct ProfRec {
     int kind;            // -1 frame begin, 0 camera, 1 intersect, 2 shade, 3 compact scatter,
                          // 4 material sort, 5 compact count+scan, 100+b fused bounce b,
-                         // 200+b its split BVH traversal kernel
+                         // 200+b its split BVH traversal kernel, 300+b k_tail from bounce b
     hipEvent_t start, stop;
 };
 // The per-dispatch events skip the system-scope fence a default event performs when it is
@@ -1051,7 +1054,7 @@ int enqueue_pass_body(int batch) {
         if (t) {
             constexpr int V = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST;
             const size_t lds = sizeof(DevGeomHot) * g.sc.num_geoms + sizeof(BlockLds);
-            launch(100 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
+            launch(300 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
                    g.seg_stride, depth);
             HIPCHK(hipGetLastError());
         }
@@ -1124,6 +1127,7 @@ int build_graph(int batch) {
 
 // one pass: frames iter .. iter + batch - 1
 int run_pass(int iter, int batch) {
+    RC(ensure_frames(batch));
     if (g.opts.use_graph) {
         if (!g.graph_exec[batch]) RC(build_graph(batch));
         // the graph's k_frame_begin increments: preset iter - 1 (stream-ordered)
@@ -1188,18 +1192,129 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
     return h;
 }
 
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+// staged-pipeline buffers (hits, alive flags, permutation, tile counts): the staged pipeline and
+// the pt_test_* entry points use them; the fused pipeline never does
+void free_staged_buffers() {
+    dfree(g.d_hit_nt);
+    dfree(g.d_hit_mat);
+    dfree(g.d_hit_uvd0);
+    dfree(g.d_hit_uvd1);
+    dfree(g.d_alive);
+    dfree(g.d_perm);
+    dfree(g.d_tile_hist);
+    dfree(g.d_tile_cnt);
+    dfree(g.d_tile_off);
+    g.staged_alloc = false;
+}
+void free_pass_buffers() {
+    free_staged_buffers();
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k) dfree(g.d_path[i][k]);
+    dfree(g.queue.A);
+    dfree(g.queue.B);
+    dfree(g.queue.C);
+    dfree(g.queue.D);
+    dfree(g.d_contrib);
+    g.sc.contrib = nullptr;
+    g.alloc_frames = 0;
+    g.seg_stride = 0;
+    g.capacity = 0;
+}
+
+// output segment s receives the survivors of the chunks c = s (mod NSEG): of k_bounce's, and in
+// split mode also of k_bvh_bounce's (its chunks of the queue) -- twice the room then
+int seg_stride_for(int frames) {
+    const int nb = nblocks(std::max(1, g.local_pixels * frames));
+    return ((nb + NSEG - 1) / NSEG) * BLOCK * (g.split ? 2 : 1);
+}
+// paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
+int capacity_for(int frames) {
+    const int c = std::max(seg_stride_for(frames) * NSEG, g.local_pixels * frames);
+    return ((c + STILE - 1) / STILE) * STILE;
+}
+// device bytes of the per-pass buffers for `frames` frames (auto F is capped by free memory)
+size_t pass_bytes(int frames, bool staged) {
+    const size_t cap = (size_t)capacity_for(frames);
+    size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
+    if (g.split) b += 4 * sizeof(float4) * (size_t)g.local_pixels * frames;       // traversal queue
+    if (frames > 1) b += 3 * sizeof(float) * (size_t)g.pixels_total * frames;      // contribution planes
+    if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (g.num_tex ? 2 * sizeof(float4) : 0));
+    return b;
+}
+
+// Path buffers, traversal queue and contribution planes for passes of up to `frames` frames.
+// Grows only; captured pass graphs hold the old pointers, so they are released on growth.
+int ensure_frames(int frames) {
+    frames = std::max(1, frames);
+    if (frames <= g.alloc_frames) return PT_OK;
+    const bool staged = g.staged_alloc || g.opts.pipeline == PT_PIPELINE_STAGED;
+    release_graph();
+    HIPCHK(hipStreamSynchronize(g.stream));
+    free_pass_buffers();
+    g.seg_stride = seg_stride_for(frames);
+    g.capacity = capacity_for(frames);
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
+    if (g.split) {
+        const size_t qn = (size_t)g.local_pixels * frames;
+        RC(dalloc(&g.queue.A, qn));
+        RC(dalloc(&g.queue.B, qn));
+        RC(dalloc(&g.queue.C, qn));
+        RC(dalloc(&g.queue.D, qn));
+    }
+    if (frames > 1) RC(dalloc(&g.d_contrib, (size_t)g.pixels_total * 3 * frames));
+    g.sc.contrib = g.d_contrib;
+    g.alloc_frames = frames;
+    if (staged) {
+        RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
+        RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
+        if (g.num_tex) {
+            RC(dalloc(&g.d_hit_uvd0, (size_t)g.capacity));
+            RC(dalloc(&g.d_hit_uvd1, (size_t)g.capacity));
+        }
+        RC(dalloc(&g.d_alive, (size_t)g.capacity));
+        RC(dalloc(&g.d_perm, (size_t)g.capacity));
+        const int ntiles = (g.capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
+        RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, g.sc.num_mats)));
+        RC(dalloc(&g.d_tile_cnt, (size_t)ntiles));
+        RC(dalloc(&g.d_tile_off, (size_t)ntiles));
+        g.staged_alloc = true;
+    }
+    return PT_OK;
+}
+// the staged buffers at the current capacity (the pt_test_* entry points under the fused pipeline)
+int ensure_staged() {
+    if (g.staged_alloc) return PT_OK;
+    const int f = std::max(1, g.alloc_frames);
+    g.alloc_frames = 0;              // re-size everything with the staged buffers included
+    g.staged_alloc = true;
+    return ensure_frames(f);
+}
+// a pt_test_* call on n paths: room for n (up to what a pass of g.batch frames holds) + staged buffers
+int ensure_test_paths(int64_t n) {
+    const int64_t most = capacity_for(g.batch);
+    if (n < 0 || n > most) return fail(PT_E_INVALID, "n out of range (capacity %lld)", (long long)most);
+    RC(ensure_staged());
+    const int frames = (int)std::min<int64_t>(g.batch, std::max<int64_t>(1, (n + g.local_pixels - 1) / g.local_pixels));
+    RC(ensure_frames(frames));
+    if (n > g.capacity) return fail(PT_E_INVALID, "n out of range (capacity %d)", g.capacity);
+    return PT_OK;
+}
+
 void free_all() {
     release_graph();
-    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_quads, g.d_hot4, g.d_leaf9, g.d_cold, g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1, g.d_texels, g.d_texinfo, g.d_alive,
-                    g.d_perm, g.d_tile_hist, g.d_tile_cnt, g.d_tile_off, g.d_image, g.d_contrib, g.d_ctl,
-                    g.queue.A, g.queue.B, g.queue.C, g.queue.D};
+    free_pass_buffers();
+    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_quads, g.d_hot4,
+                    g.d_leaf9, g.d_cold, g.d_texels, g.d_texinfo, g.d_image, g.d_ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    for (int i = 0; i < 2; ++i)
-        for (int k = 0; k < 3; ++k)
-            if (g.d_path[i][k]) (void)hipFree(g.d_path[i][k]);
     if (g.stream) (void)hipStreamDestroy(g.stream);
-    if (g.host_reg) (void)hipHostUnregister(g.host_reg);
     int32_t* td = g.traced_depth;
     g = State();
     g.traced_depth = td;
@@ -1365,8 +1480,6 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     g.local_pixels = sh.local_pixels;
     if (o.frames_per_pass < 0 || o.frames_per_pass > MAXF)
         return fail(PT_E_INVALID, "frames_per_pass must be 0 (auto) .. %d", MAXF);
-    g.batch = o.frames_per_pass > 0 ? o.frames_per_pass : auto_batch(g.local_pixels);
-    if ((int64_t)g.local_pixels * g.batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
 
     // ---- scene -> device records ----
     std::vector<DevGeom> geoms(s->num_geoms);
@@ -1837,12 +1950,20 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                             v, first ? "camera" : "later");
         }
     }
-    const int nb = nblocks(std::max(1, g.local_pixels * g.batch));
-    // output segment s receives the survivors of the chunks c = s (mod NSEG): of k_bounce's, and
-    // in split mode also of k_bvh_bounce's (its chunks of the queue) -- twice the room then
-    g.seg_stride = ((nb + NSEG - 1) / NSEG) * BLOCK * (g.split ? 2 : 1);
-    g.capacity = std::max(g.seg_stride * NSEG, g.local_pixels * g.batch);
-    g.capacity = ((g.capacity + STILE - 1) / STILE) * STILE;   // tile-padded: kernels may read a whole tile
+    g.num_tex = (s->num_textures > 0 && s->textures) ? s->num_textures : 0;
+    g.sc.num_mats = s->num_materials;
+    // frames per pass: as asked, or auto (~84M paths), halved while the per-pass buffers would
+    // take more than half of the device memory free now.  Buffers are allocated when a pass of
+    // that size is first traced or prepared (ensure_frames), not here.
+    if (o.frames_per_pass > 0) {
+        g.batch = o.frames_per_pass;
+    } else {
+        g.batch = auto_batch(g.local_pixels);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            while (g.batch > 1 && pass_bytes(g.batch, o.pipeline == PT_PIPELINE_STAGED) > free_b / 2) g.batch /= 2;
+    }
+    if ((int64_t)g.local_pixels * g.batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
 
     RC(dalloc(&g.d_geoms, geoms.size()));
     RC(dalloc(&g.d_mats, mats.size()));
@@ -1872,17 +1993,6 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             RC(upload(g.d_leaf9, leaf9.data(), leaf9.size()));
         }
     }
-    for (int i = 0; i < 2; ++i)
-        for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
-    if (g.split) {
-        const size_t qn = (size_t)g.local_pixels * g.batch;
-        RC(dalloc(&g.queue.A, qn));
-        RC(dalloc(&g.queue.B, qn));
-        RC(dalloc(&g.queue.C, qn));
-        RC(dalloc(&g.queue.D, qn));
-    }
-    RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
-    RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
     int num_tex = 0;
     if (s->num_textures > 0 && s->textures) {
@@ -1903,18 +2013,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             HIPCHK(smemcpy(g.d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
         }
         RC(upload(g.d_texinfo, info.data(), info.size()));
-        RC(dalloc(&g.d_hit_uvd0, (size_t)g.capacity));
-        RC(dalloc(&g.d_hit_uvd1, (size_t)g.capacity));
         num_tex = s->num_textures;
     }
-    RC(dalloc(&g.d_alive, (size_t)g.capacity));
-    RC(dalloc(&g.d_perm, (size_t)g.capacity));
-    const int ntiles = (g.capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
-    RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, s->num_materials)));
-    RC(dalloc(&g.d_tile_cnt, (size_t)ntiles));
-    RC(dalloc(&g.d_tile_off, (size_t)ntiles));
     RC(dalloc(&g.d_image, (size_t)g.pixels_total * 3));
-    if (g.batch > 1) RC(dalloc(&g.d_contrib, (size_t)g.pixels_total * 3 * g.batch));
     HIPCHK(smemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
     RC(dalloc(&g.d_ctl, 1));
     HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
@@ -1957,6 +2058,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     // bounds from s = sx on the device, rounded up
     sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
     sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
+    RC(ensure_frames(1));            // one frame's wavefront now; larger passes grow it on first use
     g.inited = true;
     HIPCHK(hipDeviceSynchronize());
     return PT_OK;
@@ -1985,18 +2087,11 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         HIPCHK(hipGetLastError());
     }
     if (host_image) {
+        // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
+        // page-locked: a registration would outlive a caller that frees the buffer and gets a new
+        // one at the same address, and on MI355X the pageable copy runs at the pinned rate anyway
+        // (tools/copy_probe.py: 7.68 MB in 0.145 ms either way)
         const size_t bytes = sizeof(float) * 3 * (size_t)g.pixels_total;
-        if (g.host_reg != host_image || g.host_reg_bytes != bytes) {
-            if (g.host_reg) (void)hipHostUnregister(g.host_reg);
-            g.host_reg = nullptr;
-            // pageable memory the caller owns; when it cannot be registered the copy still works
-            if (hipHostRegister(host_image, bytes, hipHostRegisterDefault) == hipSuccess) {
-                g.host_reg = host_image;
-                g.host_reg_bytes = bytes;
-            } else {
-                (void)hipGetLastError();
-            }
-        }
         HIPCHK(hipMemcpyAsync(host_image, g.d_image, bytes, hipMemcpyDeviceToHost, g.stream));
     }
     HIPCHK(hipStreamSynchronize(g.stream));
@@ -2036,6 +2131,7 @@ int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
 int32_t pt_prepare_frames(int32_t count) {
     RC(need_init());
     if (count < 0) return fail(PT_E_INVALID, "bad count");
+    RC(ensure_frames(count > 0 ? pass_frames(count) : 1));   // the largest pass of the run comes first
     if (!g.opts.use_graph) return PT_OK;
     // the pass sizes pt_trace_frames(., count) will replay
     for (int i = 0; i < count;) {
@@ -2125,6 +2221,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
         int64_t cur = 0;
         for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k][0];
         out->live_total[b] = (int64_t)ctl.tot[b] + (ctl.frames > 0 ? cur : 0);
+        out->queued_total[b] = (int64_t)ctl.qtot[b] + (ctl.frames > 0 ? ctl.qcnt[b][0] : 0);
         if (b < out->bounces) out->segments_total += out->live_total[b];
     }
     return PT_OK;
@@ -2143,6 +2240,7 @@ int32_t pt_reset_stats(void) {
 int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(need_init());
     if (!out || n < g.local_pixels) return fail(PT_E_INVALID, "output too small");
+    RC(ensure_frames(1));
     HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
     hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels, 1);
     hipLaunchKernelGGL(k_camera, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
@@ -2156,18 +2254,26 @@ int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
 
 int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_isect* isects) {
     RC(need_init());
-    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range (capacity %d)", g.capacity);
+    RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
     RC(set_count(0, (int)n));
     // uv / dpdu / dpdv are kept by the production pipelines only for textured scenes (nothing else
     // reads them); this entry point returns the reference's whole record, so mesh scenes without
-    // textures get temporary attribute buffers
+    // textures get temporary attribute buffers, released on every return path
+    struct TmpAttr {
+        float4* p[2] = {nullptr, nullptr};
+        ~TmpAttr() {
+            for (float4* x : p)
+                if (x) (void)hipFree(x);
+        }
+    } tmp;
     float4 *uvd0 = g.d_hit_uvd0, *uvd1 = g.d_hit_uvd1;
-    const bool tmp_attr = !uvd0 && g.has_bvh;
-    if (tmp_attr) {
-        RC(dalloc(&uvd0, (size_t)n));
-        RC(dalloc(&uvd1, (size_t)n));
+    if (!uvd0 && g.has_bvh) {
+        RC(dalloc(&tmp.p[0], (size_t)n));
+        RC(dalloc(&tmp.p[1], (size_t)n));
+        uvd0 = tmp.p[0];
+        uvd1 = tmp.p[1];
     }
     HitBuf hits{g.d_hit_nt, g.d_hit_mat, uvd0, uvd1};
     if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
@@ -2192,10 +2298,6 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
         HIPCHK(smemcpy(a0.data(), uvd0, n * sizeof(float4), hipMemcpyDeviceToHost));
         HIPCHK(smemcpy(a1.data(), uvd1, n * sizeof(float4), hipMemcpyDeviceToHost));
     }
-    if (tmp_attr) {
-        (void)hipFree(uvd0);
-        (void)hipFree(uvd1);
-    }
     for (int64_t i = 0; i < n; ++i) {
         memset(&isects[i], 0, sizeof(pt_shadeable_isect));
         isects[i].t = nt[i].w;
@@ -2214,7 +2316,7 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
 
 int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_path_segment* paths, int64_t n) {
     RC(need_init());
-    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
     RC(set_count(0, (int)n));
@@ -2253,7 +2355,7 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
 
 int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment* out, int64_t* alive_out) {
     RC(need_init());
-    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    RC(ensure_test_paths(n));
     RC(upload_paths(0, paths, n));
     std::vector<int> al(std::max<int64_t>(1, n));
     for (int64_t i = 0; i < n; ++i) al[i] = paths[i].remainingBounces > 0;   // PathAlive
@@ -2276,7 +2378,7 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
 
 int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm) {
     RC(need_init());
-    if (n < 0 || n > g.capacity) return fail(PT_E_INVALID, "n out of range");
+    RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
     const int nk = std::max(1, g.sc.num_mats);
     std::vector<int> mat(n);
@@ -2355,6 +2457,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     RC(need_init());
     if (!out || count <= 0) return fail(PT_E_INVALID, "bad arguments");
     memset(out, 0, sizeof(*out));
+    RC(ensure_frames(pass_frames(count)));
     // the same passes as pt_trace_frames, launched eagerly with per-dispatch start/stop events,
     // no host synchronisation until the end; stream-level events around the whole run
     std::vector<ProfRec> rec;
@@ -2388,7 +2491,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     hipError_t se = hipStreamSynchronize(g.stream);
     const int passes = (int)pass_start.size();
     double bounce_ms[MAXB] = {0}, bvh_ms[MAXB] = {0};
-    double compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0, scan_ms = 0, comb_ms = 0;
+    double compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0, scan_ms = 0, comb_ms = 0, tail_ms = 0;
+    int tail_from = 0;
     float frame_ms = 0;
     if (rc == PT_OK && se == hipSuccess) {
         (void)hipEventElapsedTime(&frame_ms, e0, e1);
@@ -2399,7 +2503,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, rec[i].start, rec[i].stop);
                 int k = rec[i].kind;
-                if (k >= 200) { bounce_ms[k - 200] += ms; bvh_ms[k - 200] += ms; }
+                if (k >= 300) { tail_ms += ms; tail_from = k - 300; }
+                else if (k >= 200) { bounce_ms[k - 200] += ms; bvh_ms[k - 200] += ms; }
                 else if (k >= 100) bounce_ms[k - 100] += ms;
                 else if (k == 0) cam_ms += ms;
                 else if (k == 1) isect_ms += ms;
@@ -2432,6 +2537,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     out->camera_ms = (float)(cam_ms / count);
     out->sort_ms = (float)(sort_ms / count);
     out->compact_scan_ms = (float)(scan_ms / count);
+    out->tail_ms = (float)(tail_ms / passes);
+    out->tail_from = tail_from;
     return PT_OK;
 }
 

@@ -30,18 +30,20 @@ std::vector<unsigned char> to_rgb8(const std::vector<pt_vec3>& image, int width,
 }
 
 namespace {
-uint32_t crc_table[256];
-bool crc_init = false;
-uint32_t crc32(const unsigned char* buf, size_t n, uint32_t c = 0xffffffffu) {
-    if (!crc_init) {
+// CRC-32 table built at compile time (pt_save_png may run on several threads at once)
+struct CrcTable {
+    uint32_t t[256];
+    constexpr CrcTable() : t() {
         for (uint32_t i = 0; i < 256; i++) {
             uint32_t k = i;
             for (int j = 0; j < 8; j++) k = (k & 1) ? 0xedb88320u ^ (k >> 1) : k >> 1;
-            crc_table[i] = k;
+            t[i] = k;
         }
-        crc_init = true;
     }
-    for (size_t i = 0; i < n; i++) c = crc_table[(c ^ buf[i]) & 0xff] ^ (c >> 8);
+};
+constexpr CrcTable crc_table{};
+uint32_t crc32(const unsigned char* buf, size_t n, uint32_t c = 0xffffffffu) {
+    for (size_t i = 0; i < n; i++) c = crc_table.t[(c ^ buf[i]) & 0xff] ^ (c >> 8);
     return c;
 }
 void put32(std::vector<unsigned char>& v, uint32_t x) {

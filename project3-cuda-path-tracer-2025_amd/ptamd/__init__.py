@@ -73,7 +73,8 @@ class _FrameStats(ctypes.Structure):
     _fields_ = [("iteration", ctypes.c_int32), ("bounces", ctypes.c_int32), ("live", ctypes.c_int64 * 64),
                 ("segments", ctypes.c_int64), ("pixels", ctypes.c_int64), ("frames_total", ctypes.c_int64),
                 ("live_total", ctypes.c_int64 * 65), ("segments_total", ctypes.c_int64),
-                ("frames_per_pass", ctypes.c_int32), ("last_pass_frames", ctypes.c_int32)]
+                ("frames_per_pass", ctypes.c_int32), ("last_pass_frames", ctypes.c_int32),
+                ("queued_total", ctypes.c_int64 * 65)]
 
 
 class _KernelTimes(ctypes.Structure):
@@ -81,7 +82,8 @@ class _KernelTimes(ctypes.Structure):
                 ("compact_ms", ctypes.c_float), ("intersect_ms", ctypes.c_float), ("shade_ms", ctypes.c_float),
                 ("camera_ms", ctypes.c_float), ("sort_ms", ctypes.c_float), ("compact_bytes", ctypes.c_int64),
                 ("frame_bytes", ctypes.c_int64), ("compact_scan_ms", ctypes.c_float), ("passes", ctypes.c_int32),
-                ("combine_ms", ctypes.c_float), ("bvh_ms", ctypes.c_float * 64)]
+                ("combine_ms", ctypes.c_float), ("bvh_ms", ctypes.c_float * 64), ("tail_ms", ctypes.c_float),
+                ("tail_from", ctypes.c_int32)]
 
 
 # every symbol the C-ABI header declares (tests check the library exports all of them)
@@ -303,8 +305,7 @@ class PathTracer:
         self.iteration = self.iteration + 1 if iteration is None else int(iteration)
         img = None
         if copy_image:
-            # one host buffer per tracer, like the reference's scene->state.image: the library
-            # page-locks it on first use (the pointer must stay the same allocation)
+            # one host buffer per tracer, like the reference's scene->state.image
             if self._host_image is None:
                 self._host_image = np.empty((self.pixels, 3), np.float32)
             img = self._host_image
@@ -343,7 +344,8 @@ class PathTracer:
                 "segments": s.segments, "pixels": s.pixels, "frames_total": s.frames_total,
                 "live_total": [s.live_total[i] for i in range(s.bounces + 1)],
                 "segments_total": s.segments_total, "frames_per_pass": s.frames_per_pass,
-                "last_pass_frames": s.last_pass_frames}
+                "last_pass_frames": s.last_pass_frames,
+                "queued_total": [s.queued_total[i] for i in range(s.bounces + 1)]}
 
     def reset_stats(self):
         _check(lib.pt_reset_stats(), "pt_reset_stats")
@@ -356,7 +358,8 @@ class PathTracer:
                 "bounce_ms": [t.bounce_ms[i] for i in range(max(1, self.trace_depth))],
                 "bvh_ms": [t.bvh_ms[i] for i in range(max(1, self.trace_depth))],
                 "compact_ms": t.compact_ms, "intersect_ms": t.intersect_ms, "shade_ms": t.shade_ms,
-                "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms}
+                "camera_ms": t.camera_ms, "sort_ms": t.sort_ms, "compact_scan_ms": t.compact_scan_ms,
+                "tail_ms": t.tail_ms, "tail_from": t.tail_from}
 
     SECTIONS = ["load", "cull", "exact", "finish", "shade", "store", "n_exact", "n_cand", "n_iters", "n_waves",
                 "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers"]
@@ -399,7 +402,7 @@ class PathTracer:
         return perm
 
     def free(self):
-        lib.pt_free()               # also releases the page-locked host image
+        lib.pt_free()
         self._host_image = None
         if PathTracer._live is self:
             PathTracer._live = None

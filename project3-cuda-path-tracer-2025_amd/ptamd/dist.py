@@ -75,21 +75,36 @@ class TileGather:
         self.bufs = [torch.empty_like(self.tile) for _ in range(world)] if rank == 0 else None
         self.device = device
 
+    def _image(self):
+        import torch
+        if self.backend == "nccl":
+            return device_image(self.tr, self.device).view(self.shape)
+        return torch.from_numpy(self.tr.image()).view(self.shape)
+
+    def pack(self):
+        """This rank's rows of the framebuffer into the packed tile (on the device with RCCL)."""
+        self._img = self._image()
+        own = self.idx[self.rank]
+        self.tile[:len(own)] = self._img.index_select(0, own)
+        return self.tile
+
+    def unpack(self, tiles):
+        """Rank 0: write every other rank's packed tile into the framebuffer's rows, in place."""
+        for r in range(1, self.world):
+            self._img.index_copy_(0, self.idx[r], tiles[r][:len(self.idx[r])])
+        if self.backend != "nccl":
+            self.tr.set_image(self._img.numpy().reshape(-1, 3))
+
     def run(self):
         import torch
         import torch.distributed as dist
-        if self.backend == "nccl":
-            img = device_image(self.tr, self.device).view(self.shape)
-        else:
-            img = torch.from_numpy(self.tr.image()).view(self.shape)
-        own = self.idx[self.rank]
-        self.tile[:len(own)] = img.index_select(0, own)
+        self.pack()
         dist.gather(self.tile, self.bufs, dst=0)
         if self.rank == 0:
-            for r in range(1, self.world):
-                img.index_copy_(0, self.idx[r], self.bufs[r][:len(self.idx[r])])
-            if self.backend != "nccl":
-                self.tr.set_image(img.numpy().reshape(-1, 3))
+            self.unpack(self.bufs)
+        if self.backend == "nccl":
+            # the library's own stream reads the framebuffer next: finish torch's writes first
+            torch.cuda.current_stream().synchronize()
 
 
 class ImageReduce:
@@ -102,6 +117,7 @@ class ImageReduce:
         import torch
         if self.backend == "nccl":
             combine(device_image(self.tr, self.device))
+            torch.cuda.current_stream().synchronize()
         else:
             img = torch.from_numpy(self.tr.image().reshape(-1))
             combine(img)

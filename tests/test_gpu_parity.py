@@ -146,14 +146,22 @@ def test_stable_compaction(n, frac, oracle, ptamd):
     tr.free()
 
 
-@pytest.mark.parametrize("nkeys,n", [(5, 10000), (27, 70000), (1, 3000), (7, 2049)])
+@pytest.mark.parametrize("nkeys,n", [(5, 10000), (27, 70000), (1, 3000), (7, 2049), (27, 20_000_003),
+                                     (5, 30_720_000)])
 def test_material_sort_stable(nkeys, n, ptamd, oracle):
+    """k_sort_hist / k_sort_scan / k_sort_scatter == np.argsort(kind="stable") (thrust::
+    stable_sort_by_key, pathtrace.cu:730-735), up to the ~20-30M paths of a benched 48-frame pass:
+    there k_sort_scan's 1024 threads each scan a run of ~260 (key, tile) entries."""
     a, b = _oracle_pair(oracle, ptamd, "cornell_obj_khaslana" if nkeys > 7 else "cornell", (400, 400))
     tr = ptamd.PathTracer(b)
     rng = np.random.default_rng(nkeys)
     k = min(nkeys, len(b.materials))
     isects = np.zeros(n, ptamd.ISECT)
-    isects["materialId"] = rng.integers(0, k, n)
+    if n > 10_000_000:    # runs of equal keys as well as scattered ones
+        isects["materialId"] = np.where(rng.random(n) < 0.5, rng.integers(0, k, n),
+                                        (np.arange(n) // 4099) % k)
+    else:
+        isects["materialId"] = rng.integers(0, k, n)
     perm = tr.test_sort(isects)
     assert _eq(perm, np.argsort(isects["materialId"], kind="stable").astype(np.int32))
     tr.free()
@@ -483,6 +491,79 @@ def test_benched_configuration_bitexact(name, oracle, ptamd):
     assert st["live_total"][:a.trace_depth] == tot.tolist()
     img = tr.image()
     assert _eq(img, r.image), (name, int(np.sum(img.view(np.uint32) != r.image.view(np.uint32))))
+    tr.free()
+
+
+def test_benched_sort_configuration_bitexact(oracle, ptamd):
+    """What bench.py's configs[2] sub-record times: cornell_glass_test 800x800 depth 8, staged
+    pipeline WITH the material sort (k_sort_hist / k_sort_scan / k_sort_scatter before every
+    k_shade), auto frames per pass, 48 frames as one wavefront pass of ~30M paths.  Image and
+    per-bounce live totals == the oracle's (material_sort=1) frame by frame."""
+    a, b = _oracle_pair(oracle, ptamd, "cornell_glass_test", None)
+    tr = ptamd.PathTracer(b, pipeline=ptamd.PIPELINE_STAGED, material_sort=1)
+    tr.prepare_frames(48)
+    tr.trace_frames(1, 48)
+    st = tr.stats()
+    assert st["frames_per_pass"] >= 48 and st["last_pass_frames"] == 48 and st["frames_total"] == 48
+    r = oracle.Renderer(a, oracle.options(material_sort=1, **BIT))
+    tot = np.zeros(a.trace_depth, np.int64)
+    for it in range(1, 49):
+        tot += np.maximum(r.trace(it), 0)
+    assert st["live_total"][:a.trace_depth] == tot.tolist()
+    img = tr.image()
+    assert _eq(img, r.image), int(np.sum(img.view(np.uint32) != r.image.view(np.uint32)))
+    tr.free()
+
+
+def test_rccl_framebuffer_combine_device_branches():
+    """The RCCL (nccl backend) branches of ptamd/dist.py, which only an N-GPU run executes:
+    a world-size-1 RCCL group in a fresh child process runs TileGather.run() and
+    ImageReduce.run() on the library's HBM framebuffer, and scatters 3 pixel shards' device tiles
+    (traced one after another on this GPU) into rank 0's framebuffer through the same
+    index_select / index_copy_ code, with the tracer's host-copy methods disabled: bit-identical
+    to the unsharded frame (tests/rccl_child.py)."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "tests", "rccl_child.py"),
+                        scene_path("cornell_glass_test"), "3", "3"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["backend"] == "nccl" and out["world"] == 1
+    assert out["tilegather_run_identity"] and out["imagereduce_run_identity"]
+    assert out["shards_scatter_equal"], out
+    assert out["image_sum"] > 0
+
+
+def test_pass_buffers_sized_on_first_use(oracle, ptamd):
+    """pt_init holds one frame's wavefront (what the drop-in pathtrace() and the viewer use); a
+    pass of F frames grows the buffers when it is first prepared or traced, and the frames after the
+    growth are still bit-exact (the pass graphs captured before it are released)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")          # the HIP runtime libptamd.so runs on (not torch's)
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    a, b = _oracle_pair(oracle, ptamd, "cornell_obj_bnnuy", None)
+    free0 = free_bytes()
+    tr = ptamd.PathTracer(b)                       # auto F = 128 at 800x800
+    used_init = free0 - free_bytes()
+    assert used_init < 1.0e9, used_init             # ~0.25 GB: one frame (x2 for the split queue's segments)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr.trace(1)
+    r.trace(1)
+    tr.prepare_frames(16)
+    used_pass = free0 - free_bytes()
+    assert used_pass > 8 * used_init, (used_init, used_pass)
+    tr.trace_frames(2, 16)
+    tr.trace(18)
+    for it in range(2, 19):
+        r.trace(it)
+    assert _eq(tr.image(), r.image)
     tr.free()
 
 
