@@ -92,8 +92,10 @@ struct FrameCtl {
 // VAR_SECTION_TIMING (tools/section_times.py): wave-level s_memtime deltas per kernel section and
 // per-lane work counters, summed by the first active lane of each wave
 enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
-       SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS, SEC_COUNT };
-__device__ unsigned long long g_sections[16];
+       SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS,
+       SEC_N_LEAVES, SEC_COUNT };
+constexpr int SEC_SLOTS = 24;
+__device__ unsigned long long g_sections[SEC_SLOTS];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
 PT_DEV void sec_add(int k, uint64_t v) {
     // one atomic per wave: the first active lane adds the wave's value
@@ -460,6 +462,20 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
     const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
     if (COUNT) n_nodes++;
     const DevPair pr = sc.pairs[st.cur];
+#ifdef PT_PROBE_EXTRA_LOAD   // tools: resource probe (one more dwordx4 gather per inner step, result unused)
+    {
+        const v4f x = reinterpret_cast<const v4f*>(sc.pairs)[4 * (size_t)(st.cur ^ 1) + 1];
+        asm volatile("" ::"v"(x[0]));
+    }
+#endif
+#ifdef PT_PROBE_EXTRA_VALU   // tools: resource probe (PT_PROBE_EXTRA_VALU dependent VALU per inner step)
+    {
+        float y = pr.l_lo.x;
+#pragma unroll
+        for (int k = 0; k < PT_PROBE_EXTRA_VALU; ++k) asm volatile("v_add_f32 %0, %0, %0" : "+v"(y));
+        asm volatile("" ::"v"(y));
+    }
+#endif
     float el = 0.f, er = 0.f;
     bool pl, pb;
     if (st.wfast) {   // wave-uniform
@@ -502,7 +518,11 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
 template <bool COUNT = false>
 PT_DEV void trav_leaf(const SceneDev& sc, TravState& st, int leaf, int& n_nodes, int& n_tris) {
     const int base = 4 * leaf;
-    if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
+    if (COUNT) {
+        n_nodes++;
+        n_tris += __float_as_int(sc.hot4[base].c.z);
+        sec_add_lanes(SEC_N_LEAVES, 1);
+    }
     const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
     v4f c[9];
 #pragma unroll

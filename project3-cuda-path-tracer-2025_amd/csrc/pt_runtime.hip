@@ -2439,9 +2439,9 @@ int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4*
 
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset) {
     RC(need_init());
-    if (!out || n < 0 || n > 16) return fail(PT_E_INVALID, "bad arguments");
+    if (!out || n < 0 || n > SEC_SLOTS) return fail(PT_E_INVALID, "bad arguments");
     HIPCHK(hipStreamSynchronize(g.stream));
-    unsigned long long tmp[16];
+    unsigned long long tmp[SEC_SLOTS];
     HIPCHK(hipMemcpyFromSymbolAsync(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost, g.stream));
     HIPCHK(hipStreamSynchronize(g.stream));
     for (int i = 0; i < n; ++i) out[i] = tmp[i];

@@ -362,12 +362,12 @@ class PathTracer:
                 "tail_ms": t.tail_ms, "tail_from": t.tail_from}
 
     SECTIONS = ["load", "cull", "exact", "finish", "shade", "store", "n_exact", "n_cand", "n_iters", "n_waves",
-                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers"]
+                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers", "n_leaves"]
 
     def section_counters(self, reset: bool = True) -> dict:
         """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""
-        buf = (ctypes.c_uint64 * 16)()
-        _check(lib.pt_debug_section_counters(buf, 16, int(reset)), "pt_debug_section_counters")
+        buf = (ctypes.c_uint64 * 24)()
+        _check(lib.pt_debug_section_counters(buf, 24, int(reset)), "pt_debug_section_counters")
         return {k: int(buf[i]) for i, k in enumerate(self.SECTIONS)}
 
     # ---- single-kernel entry points (tests) ----

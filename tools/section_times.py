@@ -19,10 +19,13 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--variant", type=int, default=6)
     ap.add_argument("--res", default="")
+    ap.add_argument("--depth", type=int, default=-1)
+    ap.add_argument("--out", default="", help="also write the JSON here")
     args = ap.parse_args()
     import ptamd
     res = tuple(int(x) for x in args.res.split("x")) if args.res else None
-    sc = ptamd.SceneFile(os.path.join(REPO, "scenes", args.scene + ".json"), res=res)
+    sc = ptamd.SceneFile(os.path.join(REPO, "scenes", args.scene + ".json"), res=res,
+                         depth=args.depth if args.depth >= 0 else None)
     tr = ptamd.PathTracer(sc, variant=args.variant)
     tr.trace_frames(1, 8)
     tr.synchronize()
@@ -41,11 +44,18 @@ def main():
            "loop_iters_per_wave": round(c["n_iters"] / max(1, c["n_waves"]), 3),
            "live_lanes_per_wave": round(lanes / max(1, c["n_waves"]), 2),
            "bvh_nodes_per_ray": round(c["n_nodes"] / max(1, c["n_bvh_rays"]), 2),
+           "bvh_inner_per_ray": round((c["n_nodes"] - c["n_leaves"]) / max(1, c["n_bvh_rays"]), 2),
+           "bvh_leaves_per_ray": round(c["n_leaves"] / max(1, c["n_bvh_rays"]), 2),
+           "bvh_tris_per_leaf": round(c["n_tris"] / max(1, c["n_leaves"]), 3),
            "bvh_tris_per_ray": round(c["n_tris"] / max(1, c["n_bvh_rays"]), 2),
            "bvh_wave_iters_per_wave": round(c["n_bvh_witers"] / max(1, c["n_waves"]), 2),
            "bvh_simt_efficiency": round(c["n_nodes"] / max(1, 64 * c["n_bvh_witers"]), 3),
            "aabb_decision_mismatches": c["n_aabb_mismatch"], "raw": c}
+    out["skip_camera"] = os.environ.get("PT_SECTIONS_SKIP_CAMERA") is not None
     print(json.dumps(out, indent=1))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(out, f, indent=1)
     tr.free()
 
 
