@@ -93,7 +93,7 @@ struct FrameCtl {
 // per-lane work counters, summed by the first active lane of each wave
 enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
        SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS,
-       SEC_N_LEAVES, SEC_COUNT };
+       SEC_N_LEAVES, SEC_N_BVH_HITS, SEC_N_MISS_NODES, SEC_N_ROOT_CULLED, SEC_COUNT };
 constexpr int SEC_SLOTS = 24;
 __device__ unsigned long long g_sections[SEC_SLOTS];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
@@ -679,6 +679,7 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
     int n_nodes = 0, n_tris = 0;
     TravState st;
     trav_begin(sc, st, ro, rd, t_limit);
+    if (COUNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
     while (st.cur >= 0) {
         if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
         trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
@@ -687,6 +688,9 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
         sec_add_lanes(SEC_N_NODES, n_nodes);
         sec_add_lanes(SEC_N_TRIS, n_tris);
         sec_add_lanes(SEC_N_BVH_RAYS, 1);
+        const bool hit = st.t_hit != FLT_MAX_ && st.t_hit < t_limit;   // the mesh changes the winner
+        sec_add_lanes(SEC_N_BVH_HITS, hit ? 1 : 0);
+        sec_add_lanes(SEC_N_MISS_NODES, hit ? 0 : n_nodes);
     }
     return trav_result(st, bu, bv, btri);
 }

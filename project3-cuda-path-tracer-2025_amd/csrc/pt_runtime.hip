@@ -32,6 +32,7 @@
 
 #include "pt/pathtrace_abi.h"
 #include "pt_kernels.h"
+#include "trav_tree.h"
 
 using namespace ptd;
 
@@ -1828,8 +1829,57 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                     memcpy(&f, &w, 4);
                     return f;
                 };
+                // The hierarchy above the reference's leaves (trav_tree.h): a binned-SAH tree over
+                // them, its inner boxes the unions of their leaves' boxes, unless a leaf box has a
+                // NaN / infinite bound (the containment argument needs ordered bounds), the union
+                // differs from the reference root box, or the tree would not fit the stack.
+                // PT_BVH_TREE=ref (tools, A/B) keeps the reference's own hierarchy.
+                static const char* tree_env = getenv("PT_BVH_TREE");
+                std::vector<pth::TravInner> tt;
+                int th = 0;
+                bool sah = !(tree_env && strcmp(tree_env, "ref") == 0) && L >= 2;
+                if (sah) {
+                    std::vector<float> llo(3 * (size_t)L), lhi(3 * (size_t)L), ls(L);
+                    for (int k = 0; k < L; ++k) {
+                        const DevNode& nd = nodes[leaf_nodes[k]];
+                        llo[3 * k] = nd.lo.x; llo[3 * k + 1] = nd.lo.y; llo[3 * k + 2] = nd.lo.z;
+                        lhi[3 * k] = nd.hi.x; lhi[3 * k + 1] = nd.hi.y; lhi[3 * k + 2] = nd.hi.z;
+                        ls[k] = node_aux[leaf_nodes[k]].y;
+                    }
+                    sah = pth::build_sah_tree(llo, lhi, ls, tt, th) && th + 1 <= MAXSTACK &&
+                          (int64_t)tt.size() + L <= 65535;
+                    if (sah) {   // the union of the leaves is the reference root box, bit for bit
+                        const pth::TravChild& a = tt[0].c[0];
+                        const pth::TravChild& b = tt[0].c[1];
+                        const float r[6] = {nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z,
+                                            nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z};
+                        for (int ax = 0; ax < 3; ++ax)
+                            sah = sah && std::min(a.lo[ax], b.lo[ax]) == r[ax] && std::max(a.hi[ax], b.hi[ax]) == r[3 + ax];
+                    }
+                }
+                if (sah) {
+                    P = (int)tt.size();
+                    pairs.resize(P);
+                    for (int i = 0; i < P; ++i) {
+                        DevPair& pr = pairs[i];
+                        float4* lo[2] = {&pr.l_lo, &pr.r_lo};
+                        float4* hi[2] = {&pr.l_hi, &pr.r_hi};
+                        for (int k = 0; k < 2; ++k) {
+                            const pth::TravChild& c = tt[i].c[k];
+                            const int rf = c.leaf ? P + c.ref : c.ref;
+                            float frf;
+                            memcpy(&frf, &rf, 4);
+                            *lo[k] = make_float4(c.lo[0], c.lo[1], c.lo[2], frf);
+                            *hi[k] = make_float4(c.hi[0], c.hi[1], c.hi[2], pack_cull(c.s));
+                        }
+                    }
+                    g.stack_depth = std::max(g.stack_depth, th + 1);
+                    if (getenv("PT_BVH_TREE_INFO"))
+                        fprintf(stderr, "pt_init: SAH traversal tree over %d reference leaves, height %d (reference %d)\n", L,
+                                th, height);
+                }
                 pairs.resize(std::max(1, P));
-                for (int n = 0; n < nn; ++n) {
+                for (int n = 0; n < nn && !sah; ++n) {
                     if (id[n] < 0 || is_leaf[n]) continue;
                     const pt_bvh_node& nd = s->bvh_nodes[n];
                     DevPair& pr = pairs[id[n]];
@@ -1927,7 +1977,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         g.stack_depth = std::max(g.stack_depth, 3 * qh + 1);
                     }
                 }
-                pair_root_ref = ref(0);
+                pair_root_ref = sah ? 0 : ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;

@@ -1,0 +1,180 @@
+// trav_tree.cpp — binned-SAH traversal hierarchy over the reference's BVH leaves (trav_tree.h).
+#include "trav_tree.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+namespace pth {
+namespace {
+
+constexpr int BINS = 32;
+
+struct Box {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    void grow(const float* l, const float* h) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], (double)l[a]);
+            hi[a] = std::max(hi[a], (double)h[a]);
+        }
+    }
+    void grow(const Box& b) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], b.lo[a]);
+            hi[a] = std::max(hi[a], b.hi[a]);
+        }
+    }
+    double area() const {
+        if (!(hi[0] >= lo[0])) return 0.0;
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return x * y + y * z + z * x;
+    }
+};
+
+struct Tmp {
+    int kid[2];   // >= 0: Tmp index; < 0: -(leaf + 1)
+    float lo[3], hi[3];
+    float s;
+};
+
+}  // namespace
+
+bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>& leaf_hi,
+                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height) {
+    const int n = (int)leaf_s.size();
+    out.clear();
+    height = 0;
+    if (n < 2 || (int)leaf_lo.size() != 3 * n || (int)leaf_hi.size() != 3 * n) return false;
+    for (int i = 0; i < 3 * n; ++i)
+        if (!std::isfinite(leaf_lo[i]) || !std::isfinite(leaf_hi[i]) || leaf_lo[i] > leaf_hi[i]) return false;
+    std::vector<double> cen(3 * (size_t)n);
+    for (int i = 0; i < 3 * n; ++i) cen[i] = 0.5 * ((double)leaf_lo[i] + (double)leaf_hi[i]);
+
+    std::vector<int> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::vector<Tmp> T;
+    T.reserve(n);
+    struct Work {
+        int begin, end, parent, side, depth;
+    };
+    std::vector<Work> st{{0, n, -1, 0, 1}};
+    while (!st.empty()) {
+        const Work w = st.back();
+        st.pop_back();
+        int code;
+        if (w.end - w.begin == 1) {
+            code = -(idx[w.begin] + 1);
+            height = std::max(height, w.depth);
+        } else {
+            // centroid bounds
+            double cl[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, ch[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            for (int i = w.begin; i < w.end; ++i)
+                for (int a = 0; a < 3; ++a) {
+                    cl[a] = std::min(cl[a], cen[3 * (size_t)idx[i] + a]);
+                    ch[a] = std::max(ch[a], cen[3 * (size_t)idx[i] + a]);
+                }
+            double best = HUGE_VAL;
+            int bax = -1, bsplit = -1;
+            for (int a = 0; a < 3; ++a) {
+                const double ext = ch[a] - cl[a];
+                if (!(ext > 0.0)) continue;
+                Box bb[BINS];
+                int bc[BINS] = {0};
+                for (int i = w.begin; i < w.end; ++i) {
+                    const int k = idx[i];
+                    const int b = std::min(BINS - 1, (int)((cen[3 * (size_t)k + a] - cl[a]) / ext * BINS));
+                    bc[b]++;
+                    bb[b].grow(&leaf_lo[3 * (size_t)k], &leaf_hi[3 * (size_t)k]);
+                }
+                double rarea[BINS];
+                int rcnt[BINS];
+                Box r;
+                int rc = 0;
+                for (int b = BINS - 1; b > 0; --b) {
+                    r.grow(bb[b]);
+                    rc += bc[b];
+                    rarea[b] = r.area();
+                    rcnt[b] = rc;
+                }
+                Box l;
+                int lc = 0;
+                for (int b = 0; b < BINS - 1; ++b) {   // split after bin b
+                    l.grow(bb[b]);
+                    lc += bc[b];
+                    if (lc == 0 || rcnt[b + 1] == 0) continue;
+                    const double c = l.area() * lc + rarea[b + 1] * rcnt[b + 1];
+                    if (c < best) {
+                        best = c;
+                        bax = a;
+                        bsplit = b;
+                    }
+                }
+            }
+            int mid;
+            if (bax < 0) {   // every centroid equal: halve in index order
+                mid = w.begin + (w.end - w.begin) / 2;
+            } else {
+                const double ext = ch[bax] - cl[bax];
+                auto left = [&](int k) {
+                    return std::min(BINS - 1, (int)((cen[3 * (size_t)k + bax] - cl[bax]) / ext * BINS)) <= bsplit;
+                };
+                mid = (int)(std::stable_partition(idx.begin() + w.begin, idx.begin() + w.end, left) - idx.begin());
+                if (mid == w.begin || mid == w.end) mid = w.begin + (w.end - w.begin) / 2;
+            }
+            code = (int)T.size();
+            T.push_back(Tmp{});
+            st.push_back({mid, w.end, code, 1, w.depth + 1});
+            st.push_back({w.begin, mid, code, 0, w.depth + 1});
+        }
+        if (w.parent >= 0) T[w.parent].kid[w.side] = code;
+    }
+    // boxes and cull sizes bottom-up (children are created after their parent)
+    auto child_box = [&](int code, float* lo, float* hi, float& s) {
+        if (code < 0) {
+            const int k = -code - 1;
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = leaf_lo[3 * (size_t)k + a];
+                hi[a] = leaf_hi[3 * (size_t)k + a];
+            }
+            s = leaf_s[k];
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = T[code].lo[a];
+                hi[a] = T[code].hi[a];
+            }
+            s = T[code].s;
+        }
+    };
+    for (int i = (int)T.size() - 1; i >= 0; --i) {
+        float l0[3], h0[3], l1[3], h1[3], s0, s1;
+        child_box(T[i].kid[0], l0, h0, s0);
+        child_box(T[i].kid[1], l1, h1, s1);
+        for (int a = 0; a < 3; ++a) {
+            T[i].lo[a] = std::min(l0[a], l1[a]);   // exact: min / max of finite floats
+            T[i].hi[a] = std::max(h0[a], h1[a]);
+        }
+        T[i].s = std::max(s0, s1);
+    }
+    // breadth-first numbering (the top levels share cache lines)
+    std::vector<int> order{0}, bfs(T.size(), -1);
+    bfs[0] = 0;
+    for (size_t h = 0; h < order.size(); ++h)
+        for (int k : T[order[h]].kid)
+            if (k >= 0) {
+                bfs[k] = (int)order.size();
+                order.push_back(k);
+            }
+    out.resize(T.size());
+    for (size_t h = 0; h < order.size(); ++h) {
+        const Tmp& t = T[order[h]];
+        for (int c = 0; c < 2; ++c) {
+            TravChild& ch = out[h].c[c];
+            child_box(t.kid[c], ch.lo, ch.hi, ch.s);
+            ch.leaf = t.kid[c] < 0;
+            ch.ref = ch.leaf ? -t.kid[c] - 1 : bfs[t.kid[c]];
+        }
+    }
+    return true;
+}
+
+}  // namespace pth

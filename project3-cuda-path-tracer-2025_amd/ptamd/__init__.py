@@ -362,7 +362,8 @@ class PathTracer:
                 "tail_ms": t.tail_ms, "tail_from": t.tail_from}
 
     SECTIONS = ["load", "cull", "exact", "finish", "shade", "store", "n_exact", "n_cand", "n_iters", "n_waves",
-                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers", "n_leaves"]
+                "n_lanes", "n_nodes", "n_tris", "n_bvh_rays", "n_aabb_mismatch", "n_bvh_witers", "n_leaves",
+                "n_bvh_hits", "n_miss_nodes", "n_root_culled"]
 
     def section_counters(self, reset: bool = True) -> dict:
         """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""

@@ -47,6 +47,10 @@ def main():
            "bvh_inner_per_ray": round((c["n_nodes"] - c["n_leaves"]) / max(1, c["n_bvh_rays"]), 2),
            "bvh_leaves_per_ray": round(c["n_leaves"] / max(1, c["n_bvh_rays"]), 2),
            "bvh_tris_per_leaf": round(c["n_tris"] / max(1, c["n_leaves"]), 3),
+           "bvh_rays_winning_mesh": round(c["n_bvh_hits"] / max(1, c["n_bvh_rays"]), 4),
+           "bvh_nodes_per_losing_ray": round(c["n_miss_nodes"] / max(1, c["n_bvh_rays"] - c["n_bvh_hits"]), 2),
+           "bvh_nodes_per_winning_ray": round((c["n_nodes"] - c["n_miss_nodes"]) / max(1, c["n_bvh_hits"]), 2),
+           "bvh_rays_root_culled": round(c["n_root_culled"] / max(1, c["n_bvh_rays"]), 4),
            "bvh_tris_per_ray": round(c["n_tris"] / max(1, c["n_bvh_rays"]), 2),
            "bvh_wave_iters_per_wave": round(c["n_bvh_witers"] / max(1, c["n_waves"]), 2),
            "bvh_simt_efficiency": round(c["n_nodes"] / max(1, 64 * c["n_bvh_witers"]), 3),
