@@ -53,8 +53,9 @@ N_CUS = 256                    # MI355X compute units
 
 # BASELINE.json configs[2..4] as sub-records of the N=1 line: (tag, scene, res, depth, sort, pipeline, steps, warmup)
 SUB_CONFIGS = [
-    ("configs[2]", "cornell_glass_test.json", None, None, True, "staged", 48, 4),
-    ("configs[2] fused", "cornell_glass_test.json", None, None, False, "fused", 64, 8),
+    ("configs[2]", "cornell_glass_test.json", None, None, True, "fused", 48, 4),
+    ("configs[2] staged", "cornell_glass_test.json", None, None, True, "staged", 48, 4),
+    ("configs[2] sort off", "cornell_glass_test.json", None, None, False, "fused", 48, 4),
     ("configs[3]", "cornell_obj_bnnuy.json", None, None, False, "fused", 48, 4),
     ("configs[4]", "cornell_obj_khaslana.json", (1600, 1600), 12, False, "fused", 32, 2),
 ]
@@ -257,10 +258,11 @@ def main():
 
 def workload_str(name, w, h, depth, sort, pipeline):
     if sort and pipeline == "fused":
-        s = ("material sort requested: the fused pipeline shades each path in registers right after its "
-             "intersection, so there is nothing to sort (results are order-independent); --pipeline staged runs it")
+        s = "material sort on (block-local regrouping by material between intersection and shading)"
+    elif sort:
+        s = "material sort on (stable counting sort of the wavefront by material)"
     else:
-        s = f"sort {'on' if sort else 'off'}"
+        s = "sort off"
     return f"{name} {w}x{h} depth {depth}, stream compaction on, {s}"
 
 

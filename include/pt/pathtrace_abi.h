@@ -60,11 +60,13 @@ enum { PT_SHARD_NONE = 0, PT_SHARD_PIXELS = 1, PT_SHARD_SAMPLES = 2 };
 
 typedef struct pt_options {
     int32_t stream_compaction;   /* STREAM_COMPACTION (pathtrace.cu:21), default 1 */
-    int32_t material_sort;       /* MATERIAL_SORTING  (pathtrace.cu:22), default 0.  Sorts the
-                                    staged pipeline's shading order by material; the fused
-                                    pipeline shades every path in registers right after its
-                                    intersection, so it has no shading order to sort (results do
-                                    not depend on path order either way) */
+    int32_t material_sort;       /* MATERIAL_SORTING  (pathtrace.cu:22), default 0.  Staged
+                                    pipeline: a stable counting sort of the wavefront by
+                                    materialId before shading (k_sort_*).  Fused pipeline: the
+                                    block's paths are regrouped by material in LDS between
+                                    intersection and shading (scenes of <= 63 materials; mesh
+                                    hits shaded by the BVH queue kernel are not regrouped).
+                                    Results do not depend on path order either way */
     int32_t bvh;                 /* BVH_ACCELERATION  (pathtrace.cu:24), default 1 */
     int32_t arg_order;           /* 0: glm::vec2(u01(rng), u01(rng)) right-to-left (g++), 1: left-to-right */
     int32_t pipeline;            /* PT_PIPELINE_FUSED (default) or PT_PIPELINE_STAGED (one kernel per stage) */

@@ -34,6 +34,8 @@ enum : int {
     VAR_BLOCK_REDIST = 128,  // with VAR_WAVE_REDIST: the exchange spans the block (block_intersect)
     VAR_BVH_QUAD = 256,    // with VAR_BVH_FAST + pair layout: traverse 4-wide nodes (DevQuad) collapsed
                            // from the binary tree (same leaves, same winner)
+    VAR_MAT_GROUP = 512,   // fused MATERIAL_SORTING: the block's paths regrouped by material between
+                           // intersection and shading (group_by_material); set by pt_options.material_sort
 };
 
 struct CamDev {
@@ -1158,6 +1160,93 @@ struct BlockLds {
     uint16_t task[BCAP];
     int wsum[BLOCK / 64];
 };
+// VAR_MAT_GROUP (MATERIAL_SORTING on the fused pipeline, pathtrace.cu:730-735 sorts the whole
+// wavefront by materialId before shading): here the block's 256 paths are regrouped by material in
+// LDS between intersection and shading, so a wave shades runs of one material.  A counting sort:
+// each wave finds the lanes that share its key with one ballot per key bit, the per-(wave, key)
+// counts are scanned over the keys by wave 0, and every thread moves its path (+ hit, + queue
+// state) to its slot.  Keys 0..MG_KEYS-1: the hit's materialId (a miss is 0, as the reference's
+// memset leaves it), MG_KEYS-1 for paths that are not shaded here.  Results do not depend on
+// which thread shades a path.
+constexpr int MG_KEYS = 64;
+constexpr int MG_WORDS = 22;   // exchanged words per path: 15, + 3 for triangle hits, + 4 for the BVH queue
+struct MatGroupLds {
+    int cnt[BLOCK / 64][MG_KEYS];
+    int off[MG_KEYS];
+    float x[MG_WORDS][BLOCK];
+};
+// bytes of MatGroupLds a kernel needs (the exchange array holds only the words it moves)
+constexpr size_t mat_group_lds(bool tri, bool split) {
+    return sizeof(int) * ((BLOCK / 64) * MG_KEYS + MG_KEYS) + sizeof(float) * BLOCK * (15 + (tri ? 3 : 0) + (split ? 4 : 0));
+}
+template <bool TRI, bool SPLIT>
+PT_DEV void group_by_material(int key, MatGroupLds* S, bool& active, bool& live, bool& queued, PathReg& p, Hit& h,
+                              float& qt, int& qw, f3& qs) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {   // MG_KEYS = 64 keys: 6 bits
+        const uint64_t bb = __ballot((key >> b) & 1);
+        peers &= ((key >> b) & 1) ? bb : ~bb;
+    }
+    for (int i = tid; i < (BLOCK / 64) * MG_KEYS; i += BLOCK) (&S->cnt[0][0])[i] = 0;
+    __syncthreads();
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+    if (below == 0) S->cnt[w][key] = __popcll(peers);
+    __syncthreads();
+    if (w == 0) {   // exclusive scan over the keys of the block totals
+        int t = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) t += S->cnt[i][lane];
+        int incl = t;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        S->off[lane] = incl - t;
+    }
+    __syncthreads();
+    int slot = S->off[key] + below;
+    for (int i = 0; i < w; ++i) slot += S->cnt[i][key];
+    // rb (0..64: 7 bits) | frame slot (8) | active, live, queued (3) | materialId (< 64: 6) | queued winner + 1 (7)
+    // (an inactive lane's path fields are unset: every field is masked to its width)
+    const uint32_t packed = ((uint32_t)p.rb & 127u) | (((uint32_t)p.slot & 255u) << 7) | ((active ? 1u : 0u) << 15) |
+                            ((live ? 1u : 0u) << 16) | ((queued ? 1u : 0u) << 17) | (((uint32_t)h.mat & 63u) << 18) |
+                            (((uint32_t)(qw + 1) & 127u) << 24);
+    constexpr int NW = 15 + (TRI ? 3 : 0) + (SPLIT ? 4 : 0);
+    float v[NW];
+    v[0] = p.o.x; v[1] = p.o.y; v[2] = p.o.z;
+    v[3] = p.d.x; v[4] = p.d.y; v[5] = p.d.z;
+    v[6] = p.c.x; v[7] = p.c.y; v[8] = p.c.z;
+    v[9] = __int_as_float(p.pix); v[10] = __uint_as_float(packed);
+    v[11] = h.t; v[12] = h.n.x; v[13] = h.n.y; v[14] = h.n.z;
+    if (TRI) { v[15] = __int_as_float(h.tri); v[16] = h.u; v[17] = h.v; }
+    if (SPLIT) { v[NW - 4] = qt; v[NW - 3] = qs.x; v[NW - 2] = qs.y; v[NW - 1] = qs.z; }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) S->x[k][slot] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NW; ++k) v[k] = S->x[k][tid];
+    p.o = mk(v[0], v[1], v[2]);
+    p.d = mk(v[3], v[4], v[5]);
+    p.c = mk(v[6], v[7], v[8]);
+    p.pix = __float_as_int(v[9]);
+    const uint32_t q = __float_as_uint(v[10]);
+    p.rb = (int)(q & 127u);
+    p.slot = (int)((q >> 7) & 255u);
+    active = ((q >> 15) & 1u) != 0;
+    live = ((q >> 16) & 1u) != 0;
+    queued = ((q >> 17) & 1u) != 0;
+    h.mat = (int)((q >> 18) & 63u);
+    qw = (int)((q >> 24) & 127u) - 1;
+    h.t = v[11];
+    h.n = mk(v[12], v[13], v[14]);
+    if (TRI) { h.tri = __float_as_int(v[15]); h.u = v[16]; h.v = v[17]; }
+    else { h.tri = -1; h.u = 0.f; h.v = 0.f; }
+    if (SPLIT) { qt = v[NW - 4]; qs = mk(v[NW - 3], v[NW - 2], v[NW - 1]); }
+}
+
 template <bool TIMING = false>
 PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, f3 ro, f3 rd, BlockLds* B,
                             float& t_min, int& win, f3& seed) {

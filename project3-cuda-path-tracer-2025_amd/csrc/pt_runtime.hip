@@ -192,7 +192,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         __syncthreads();
     }
     const int gid = block_start + tid;
-    const bool active = gid < n;
+    bool active = gid < n;
     PathReg p;
     p.rb = 0;
     if (active) {
@@ -235,8 +235,10 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             sec_add_lanes(SEC_N_LANES, p.rb > 0 ? 1 : 0);
         }
     }
-    const bool live = active && p.rb > 0;
+    bool live = active && p.rb > 0;
+    constexpr bool MG = (VAR & VAR_MAT_GROUP) != 0;
     Hit h;
+    if (MG) h = Hit{-1.f, mk(0.f, 0.f, 0.f), 0, -1, 0.f, 0.f};
     bool queued = false;
     float qt = 0.f;
     int qw = -1;
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST, FIRST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
         }
-        if (!queued) {
+        if (!MG && !queued) {
             uint64_t ts = TIMING ? sec_clock() : 0;
             shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
             if (TIMING) {
@@ -268,6 +270,25 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
                 sec_add(SEC_SHADE, tc - ts);
             }
         }
+    }
+    if (MG) {   // MATERIAL_SORTING: regroup the block's paths by material, then shade
+        if (SPLIT) {   // the rays queued for the mesh leave first, from their own threads
+            int qi, unused;
+            block_append<false>(queued, &ctl->qcnt[bounce][0], false, nullptr, qi, unused);
+            if (queued) {
+                q.A[qi] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+                q.B[qi] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+                q.C[qi] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
+                q.D[qi] = make_float4(qt, qs.x, qs.y, qs.z);
+                active = false;   // handed over to k_bvh_bounce
+                live = false;
+                queued = false;
+            }
+        }
+        const int key = live ? (h.t > 0.0f ? h.mat : 0) : MG_KEYS - 1;
+        MatGroupLds* mg = reinterpret_cast<MatGroupLds*>(s_wave_isect - (tid >> 6));
+        group_by_material<HAS_BVH, false>(key, mg, active, live, queued, p, h, qt, qw, qs);
+        if (live) shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     if (TIMING && active) tc = sec_clock();
     const bool surv = active && !queued && p.rb > 0;
@@ -945,7 +966,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
                                   ? std::max(sizeof(WaveLds) * (BLOCK / 64), (VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : 0)
                                   : 0;
     const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
-    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + redist_lds, g.sc, in, out,
+    // VAR_MAT_GROUP's exchange reuses the exact-test exchange's region (it runs after it)
+    const size_t xchg_lds = (VAR & VAR_MAT_GROUP) ? std::max(redist_lds, mat_group_lds(HAS_BVH, false)) : redist_lds;
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds, g.sc, in, out,
            g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
     // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
@@ -976,6 +999,10 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 446: launch_bounce_t<FIRST, HAS_BVH, 446>(grid, in, out, b); break;   // 442 + section counters
         case 306: launch_bounce_t<FIRST, HAS_BVH, 306>(grid, in, out, b); break;   // camera bounce of 442
         case 310: launch_bounce_t<FIRST, HAS_BVH, 310>(grid, in, out, b); break;   // camera bounce of 446
+        case 666: launch_bounce_t<FIRST, HAS_BVH, 666>(grid, in, out, b); break;   // 154 + material grouping
+        case 530: launch_bounce_t<FIRST, HAS_BVH, 530>(grid, in, out, b); break;   // camera bounce of 666
+        case 698: launch_bounce_t<FIRST, HAS_BVH, 698>(grid, in, out, b); break;   // 186 + material grouping
+        case 562: launch_bounce_t<FIRST, HAS_BVH, 562>(grid, in, out, b); break;   // camera bounce of 698
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;   // unreachable: pt_init checks
     }
 }
@@ -996,7 +1023,8 @@ int effective_variant(bool first, int var, bool has_quads) {
 // variants instantiated in launch_bounce_v (pt_init refuses others instead of running a
 // different kernel than asked for)
 bool variant_compiled(int v) {
-    static const int k[] = {0, 1, 2, 6, 10, 18, 22, 26, 30, 50, 54, 58, 154, 158, 186, 190, 306, 310, 442, 446};
+    static const int k[] = {0, 1, 2, 6, 10, 18, 22, 26, 30, 50, 54, 58, 154, 158, 186, 190, 306, 310, 442, 446,
+                            530, 562, 666, 698};
     for (int x : k)
         if (x == v) return true;
     return false;
@@ -1992,6 +2020,14 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     g.split = g.has_bvh && !pairs.empty() && o.pipeline == PT_PIPELINE_FUSED && (o.variant & VAR_BVH_SPLIT) &&
               (o.variant & VAR_BVH_FAST) && (o.variant & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) &&
               s->num_geoms <= LDS_GEOMS;
+    // MATERIAL_SORTING on the fused pipeline: the block-local regrouping by material (VAR_MAT_GROUP;
+    // keys are the material ids, at most MG_KEYS - 1 of them), for the kernel variants built with it
+    if (o.material_sort && o.pipeline == PT_PIPELINE_FUSED && s->num_materials <= MG_KEYS - 1 &&
+        variant_compiled(effective_variant(true, o.variant | VAR_MAT_GROUP, !quads.empty())) &&
+        variant_compiled(effective_variant(false, o.variant | VAR_MAT_GROUP, !quads.empty()))) {
+        o.variant |= VAR_MAT_GROUP;
+        g.opts.variant = o.variant;
+    }
     if (o.pipeline == PT_PIPELINE_FUSED) {
         for (int first = 0; first < 2; ++first) {
             const int v = effective_variant(first != 0, o.variant, !quads.empty());

@@ -215,6 +215,12 @@ FRAME_CASES = [
     ("synthetic_textured_bump", (48, 48), None, {"pipeline": 1, "material_sort": 1}),
     ("cornell_obj_phatphuck_texture_test", (48, 48), None, {}),
     ("cornell_obj_phatphuck_microfacet", (48, 48), None, {"pipeline": 1}),
+    # MATERIAL_SORTING on the fused pipeline (block-local regrouping by material, VAR_MAT_GROUP)
+    ("cornell_glass_test", (64, 64), None, {"material_sort": 1}),
+    ("cornell_multiple_glass", (64, 64), None, {"material_sort": 1}),
+    ("cornell_obj_khaslana", (48, 48), 12, {"material_sort": 1}),
+    ("synthetic_textured_bump", (48, 48), None, {"material_sort": 1}),
+    ("cornell_obj_phatphuck_microfacet", (48, 48), None, {"material_sort": 1}),
 ]
 
 
@@ -250,6 +256,8 @@ PASS_CASES = [
     ("cornell_microfacet_test", (50, 50), None, {"shard_mode": 1, "shard_rank": 1, "shard_count": 2}, 4),
     ("synthetic_textured_bump", (48, 48), None, {}, 4),
     ("cornell_multiple_glass", (64, 64), None, {"variant": 10}, 8),
+    ("cornell_multiple_glass", (64, 64), None, {"material_sort": 1}, 4),
+    ("cornell_obj_bnnuy", (48, 48), None, {"material_sort": 1}, 3),
 ]
 
 
@@ -494,13 +502,16 @@ def test_benched_configuration_bitexact(name, oracle, ptamd):
     tr.free()
 
 
-def test_benched_sort_configuration_bitexact(oracle, ptamd):
-    """What bench.py's configs[2] sub-record times: cornell_glass_test 800x800 depth 8, staged
-    pipeline WITH the material sort (k_sort_hist / k_sort_scan / k_sort_scatter before every
-    k_shade), auto frames per pass, 48 frames as one wavefront pass of ~30M paths.  Image and
-    per-bounce live totals == the oracle's (material_sort=1) frame by frame."""
+@pytest.mark.parametrize("pipeline", ["fused", "staged"])
+def test_benched_sort_configuration_bitexact(pipeline, oracle, ptamd):
+    """What bench.py's configs[2] sub-records time: cornell_glass_test 800x800 depth 8 WITH the
+    material sort -- fused (the block-local regrouping by material between intersection and
+    shading) and staged (k_sort_hist / k_sort_scan / k_sort_scatter before every k_shade) --, auto
+    frames per pass, 48 frames as one wavefront pass of ~30M paths.  Image and per-bounce live
+    totals == the oracle's (material_sort=1) frame by frame."""
     a, b = _oracle_pair(oracle, ptamd, "cornell_glass_test", None)
-    tr = ptamd.PathTracer(b, pipeline=ptamd.PIPELINE_STAGED, material_sort=1)
+    tr = ptamd.PathTracer(b, pipeline=ptamd.PIPELINE_STAGED if pipeline == "staged" else ptamd.PIPELINE_FUSED,
+                          material_sort=1)
     tr.prepare_frames(48)
     tr.trace_frames(1, 48)
     st = tr.stats()
