@@ -295,7 +295,10 @@ PT_DEV float geom_test(const DevGeomHot& g, f3 ro, f3 rd, f3& seed) {
     f3 s = mk(0.f, 0.f, 0.f);
     if (g.type == PT_CUBE) {
         float tmin = -1e38f, tmax = 1e38f;
-        f3 tmin_n = mk(0.f, 0.f, 0.f), tmax_n = mk(0.f, 0.f, 0.f);
+        // the slab normals tmin_n / tmax_n are +-1 on one axis and +0 elsewhere (or all +0): carried
+        // as a code (axis + 1) * sign, decoded to the same bits at the end -- 2 registers, not 6, at
+        // the fused kernel's peak register pressure (this runs inside the exact-test exchange)
+        int tmin_c = 0, tmax_c = 0;
 #pragma unroll
         for (int xyz = 0; xyz < 3; ++xyz) {
             float qdx = comp(qd, xyz), qox = comp(qo, xyz);
@@ -303,15 +306,16 @@ PT_DEV float geom_test(const DevGeomHot& g, f3 ro, f3 rd, f3& seed) {
             float t2 = (+0.5f - qox) / qdx;
             float ta = gmin(t1, t2);
             float tb = gmax(t1, t2);
-            float sg = t2 < t1 ? +1.0f : -1.0f;
-            f3 n = mk(xyz == 0 ? sg : 0.f, xyz == 1 ? sg : 0.f, xyz == 2 ? sg : 0.f);
-            if (ta > 0 && ta > tmin) { tmin = ta; tmin_n = n; }
-            if (tb < tmax) { tmax = tb; tmax_n = n; }
+            const int nc = t2 < t1 ? xyz + 1 : -(xyz + 1);
+            if (ta > 0 && ta > tmin) { tmin = ta; tmin_c = nc; }
+            if (tb < tmax) { tmax = tb; tmax_c = nc; }
         }
         hit = tmax >= tmin && tmax > 0;
-        if (tmin <= 0) { tmin = tmax; tmin_n = tmax_n; }
+        if (tmin <= 0) { tmin = tmax; tmin_c = tmax_c; }
         tq = tmin;
-        s = tmin_n;
+        const float sg = tmin_c > 0 ? +1.0f : -1.0f;
+        const int ax = (tmin_c < 0 ? -tmin_c : tmin_c) - 1;
+        s = mk(ax == 0 ? sg : 0.f, ax == 1 ? sg : 0.f, ax == 2 ? sg : 0.f);
     } else {
         float vDotDirection = dot(qo, qd);
         float radicand = vDotDirection * vDotDirection - (dot(qo, qo) - 0.25f);   // powf(.5, 2) == .25

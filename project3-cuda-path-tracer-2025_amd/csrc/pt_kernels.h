@@ -36,6 +36,9 @@ enum : int {
                            // from the binary tree (same leaves, same winner)
     VAR_MAT_GROUP = 512,   // fused MATERIAL_SORTING: the block's paths regrouped by material between
                            // intersection and shading (group_by_material); set by pt_options.material_sort
+    VAR_NO_TEX = 1024,     // host-set: no material samples a texture or bump map, so the fused kernels'
+                           // shading is compiled without the texel fetches (whose registers otherwise set
+                           // the kernels' VGPR count and occupancy)
 };
 
 struct CamDev {
@@ -1010,6 +1013,9 @@ PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) 
 #ifndef CULL_GROUP
 #define CULL_GROUP 4
 #endif
+#ifndef PT_DUP
+#define PT_DUP 0
+#endif
 PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
     const float4* rec = reinterpret_cast<const float4*>(sc.cull);
     const int ng = sc.num_geoms;
@@ -1151,9 +1157,16 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, 
 // of ceil(wave pairs / 64) (cornell: 79 pairs per wave on average -> 1.67 rounds each).  Same
 // per-lane scan of its own results afterwards, so the winner is unchanged.  Every thread of the
 // block must call it.
-// 768 pairs (3 per lane; cornell averages 1.2).  640 would fit one more 44-geom block per CU:
-// khaslana -0.7 %, cornell +0.8 % (A/B), so the headline keeps 768
-constexpr int BCAP = 4 * WCAP;
+// 736 pairs (2.9 per lane; cornell averages 0.93 after bounce 0): with cornell's 7-geom table the
+// block's LDS is then 20,240 B, so 8 blocks (8 waves per SIMD) fit a CU's 160 KB -- 768 needed
+// 20,816 B and held the kernel at 7 whatever its registers.  A capacity chosen per scene at run
+// time (so that khaslana's 44-geom table also fits 8 blocks, at 512 pairs) was tried: khaslana
+// +-0, cornell +1.8 % from the run-time array offsets (A/B, round 3).  (640 would fit one more
+// 44-geom block: khaslana -0.7 %, cornell +0.8 %, round 2.)
+#ifndef BCAP_PAIRS
+#define BCAP_PAIRS 736
+#endif
+constexpr int BCAP = BCAP_PAIRS;
 struct BlockLds {
     float ro[3][BLOCK], rd[3][BLOCK];
     float rt[BCAP], rs[3][BCAP];
@@ -1259,6 +1272,13 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
         cand = cull_candidates(sc, cr, ro, rd, bounded);
+#if PT_DUP == 1   // tools/valu_attrib.sh: the section's VALU counted twice (result discarded)
+        {
+            const f3 ro2 = ro + mk(0.f, 0.f, 0.f);
+            const uint64_t c2 = cull_candidates(sc, cull_ray(ro2, rd), ro2, rd, bounded);
+            asm volatile("" ::"v"((uint32_t)c2), "v"((uint32_t)(c2 >> 32)));
+        }
+#endif
     }
     const int cnt = __builtin_popcountll(cand);
     uint64_t tc1 = 0;
@@ -1282,7 +1302,10 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         woff += i < w ? x : 0;
         total += x;
     }
-    const int excl = woff + incl - cnt;
+    int excl = woff + incl - cnt;
+    // one register: left transparent, the compiler keeps the six scan partials and the four wave
+    // sums live across the exact tests and re-adds them afterwards (10 VGPRs at the peak)
+    asm volatile("" : "+v"(excl));
     t_min = FLT_MAX_;
     win = -1;
     seed = mk(0.f, 0.f, 0.f);
@@ -1322,6 +1345,13 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         const f3 d = mk(B->rd[0][src], B->rd[1][src], B->rd[2][src]);
         f3 s;
         const float t = geom_test(lg[gi], o, d, s);
+#if PT_DUP == 2
+        {
+            f3 s2;
+            const float t2 = geom_test(lg[gi], o + mk(0.f, 0.f, 0.f), d, s2);
+            asm volatile("" ::"v"(t2), "v"(s2.x), "v"(s2.y), "v"(s2.z));
+        }
+#endif
         B->rt[k] = t;
         B->rs[0][k] = s.x;
         B->rs[1][k] = s.y;
@@ -1346,7 +1376,9 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
 // (magenta for an id that names no loaded texture, pathtrace.cu:505-512) and the bump-map
 // normal perturbation (pathtrace.cu:579-607).  `attr()` yields the winner's HitAttr; it is
 // only evaluated for textured / bump-mapped materials.
-template <class AttrFn>
+// TEX = false (VAR_NO_TEX): the caller guarantees no material has hasTexture or hasBumpMap set,
+// so the texture branches below are never taken and are compiled out.
+template <bool TEX = true, class AttrFn>
 PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter, AttrFn attr) {
     if (h.t > 0.0f) {
         const DevMaterial m = sc.mats[h.mat];
@@ -1354,9 +1386,9 @@ PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter, A
         HitAttr ha;
         ha.u = ha.v = 0.0f;
         ha.dpdu = ha.dpdv = mk(0.f, 0.f, 0.f);
-        if (m.hasTexture | m.hasBumpMap) ha = attr();
+        if (TEX && (m.hasTexture | m.hasBumpMap)) ha = attr();
         const float uvx = ha.u, uvy = ha.v;
-        if (m.hasTexture) {
+        if (TEX && m.hasTexture) {
             if (m.textureID < 0 || m.textureID >= sc.num_textures) {
                 mcolor = mk(1.0f, 0.0f, 1.0f);
             } else {
@@ -1372,7 +1404,7 @@ PT_DEV void shade_path(const SceneDev& sc, PathReg& p, const Hit& h, int iter, A
             Rng rng = rng_make(iter, p.pix, p.rb);
             f3 intersect = p.o + p.d * h.t;
             f3 shadingNormal = h.n;
-            if (m.hasBumpMap && m.bumpID >= 0 && m.bumpID < sc.num_textures) {
+            if (TEX && m.hasBumpMap && m.bumpID >= 0 && m.bumpID < sc.num_textures) {
                 const f3 ng = h.n;
                 const f3 dpdu = ha.dpdu, dpdv = ha.dpdv;
                 const int4 ti = sc.texinfo[m.bumpID];

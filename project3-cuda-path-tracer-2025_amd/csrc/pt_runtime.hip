@@ -258,13 +258,28 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             if (!queued) h = finish_hit<false>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else if (REDIST && lds_geoms) {
             h = finish_hit<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
+#if PT_DUP == 4
+            {
+                const Hit h2 = finish_hit<HAS_BVH, BVH_FAST>(sc, p.o, p.d + mk(0.f, 0.f, 0.f), s_stack + tid, qt, qw, qs);
+                asm volatile("" ::"v"(h2.t), "v"(h2.n.x), "v"(h2.n.y), "v"(h2.n.z), "v"(h2.mat));
+            }
+#endif
         } else {
             h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST, FIRST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
         }
         if (!MG && !queued) {
             uint64_t ts = TIMING ? sec_clock() : 0;
-            shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+#if PT_DUP == 3
+            {
+                PathReg q = p;
+                q.c = q.c + mk(0.f, 0.f, 0.f);
+                shade_path<(VAR & VAR_NO_TEX) == 0>(sc, q, h, iter + q.slot, [&]() { return hit_attr(sc, h); });
+                asm volatile("" ::"v"(q.c.x), "v"(q.c.y), "v"(q.c.z), "v"(q.d.x), "v"(q.d.y), "v"(q.d.z), "v"(q.o.x),
+                             "v"(q.o.y), "v"(q.o.z), "v"(q.rb));
+            }
+#endif
+            shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
             if (TIMING) {
                 tc = sec_clock();
                 sec_add(SEC_SHADE, tc - ts);
@@ -288,7 +303,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         const int key = live ? (h.t > 0.0f ? h.mat : 0) : MG_KEYS - 1;
         MatGroupLds* mg = reinterpret_cast<MatGroupLds*>(s_wave_isect - (tid >> 6));
         group_by_material<HAS_BVH, false>(key, mg, active, live, queued, p, h, qt, qw, qs);
-        if (live) shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+        if (live) shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     if (TIMING && active) tc = sec_clock();
     const bool surv = active && !queued && p.rb > 0;
@@ -385,7 +400,7 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
         block_intersect<false>(sc, s_geoms, live, p.o, p.d, s_block, qt, qw, qs);
         if (live) {
             const Hit h = finish_hit<false>(sc, p.o, p.d, nullptr, qt, qw, qs);
-            shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+            shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
             if (p.rb <= 0) gather_into_image(image, sc, batch, p);
         }
         // paths entering bounce b + 1 (k_bounce's survivor count for this bounce)
@@ -411,8 +426,11 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 // vectorizer on (packed-f32 pairs built from duplicated registers) it needed 96 VGPRs for 5
 // waves; without it (Makefile) 79 VGPRs natural, and 72 at this bound (bunny 0.489 -> 0.477
 // ms/frame); 8 waves (64 VGPRs) spill 100 B
+#ifndef BVH_WAVES
+#define BVH_WAVES 7
+#endif
 template <int VAR>
-__global__ __launch_bounds__(BLOCK, 7) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
                                                       float* __restrict__ image, int bounce, int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
     const int n = ctl->qcnt[bounce][0];
@@ -446,7 +464,7 @@ __global__ __launch_bounds__(BLOCK, 7) void k_bvh_bounce(SceneDev sc, QueueBuf q
         p.slot = cw & 255;
         const int win = (cw >> 8) - 1;
         const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
-        shade_path(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+        shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     const bool surv = active && p.rb > 0;
     if (active && !surv) gather_into_image(image, sc, batch, p);
@@ -877,6 +895,7 @@ struct State {
     float* d_contrib = nullptr;      // passes of F > 1 frames: F planes of pixels_total float3
     int batch = 1;                   // frames per pass (pt_options.frames_per_pass, resolved)
     bool split = false;              // VAR_BVH_SPLIT active (fused, fast BVH on the pair layout)
+    bool no_tex = false;             // no textured / bump-mapped material (VAR_NO_TEX kernels)
     QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
@@ -962,8 +981,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
     const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && g.sc.num_geoms <= LDS_GEOMS;
     const size_t geom_lds = lds ? sizeof(DevGeomHot) * g.sc.num_geoms : 0;
+    // the exchange's region: block_intersect's BlockLds, or one WaveLds per wave (wave_intersect)
     const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds
-                                  ? std::max(sizeof(WaveLds) * (BLOCK / 64), (VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : 0)
+                                  ? ((VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : sizeof(WaveLds) * (BLOCK / 64))
                                   : 0;
     const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
     // VAR_MAT_GROUP's exchange reuses the exact-test exchange's region (it runs after it)
@@ -979,6 +999,10 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
     switch (var) {
+#ifdef PT_VAR_PROBE   // tools: register-pressure probes compile only the default variants
+        case 154: launch_bounce_t<FIRST, HAS_BVH, 154>(grid, in, out, b); break;
+        case 186: launch_bounce_t<FIRST, HAS_BVH, 186>(grid, in, out, b); break;
+#else
         case 0: launch_bounce_t<FIRST, HAS_BVH, 0>(grid, in, out, b); break;
         case 1: launch_bounce_t<FIRST, HAS_BVH, 1>(grid, in, out, b); break;
         case 2: launch_bounce_t<FIRST, HAS_BVH, 2>(grid, in, out, b); break;
@@ -1003,9 +1027,26 @@ void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
         case 530: launch_bounce_t<FIRST, HAS_BVH, 530>(grid, in, out, b); break;   // camera bounce of 666
         case 698: launch_bounce_t<FIRST, HAS_BVH, 698>(grid, in, out, b); break;   // 186 + material grouping
         case 562: launch_bounce_t<FIRST, HAS_BVH, 562>(grid, in, out, b); break;   // camera bounce of 698
+#endif
+        // the same without texture fetches (VAR_NO_TEX: no textured / bump-mapped material)
+        case 1024 + 18: launch_bounce_t<FIRST, HAS_BVH, 1024 + 18>(grid, in, out, b); break;
+        case 1024 + 22: launch_bounce_t<FIRST, HAS_BVH, 1024 + 22>(grid, in, out, b); break;
+        case 1024 + 50: launch_bounce_t<FIRST, HAS_BVH, 1024 + 50>(grid, in, out, b); break;
+        case 1024 + 54: launch_bounce_t<FIRST, HAS_BVH, 1024 + 54>(grid, in, out, b); break;
+        case 1024 + 154: launch_bounce_t<FIRST, HAS_BVH, 1024 + 154>(grid, in, out, b); break;
+        case 1024 + 158: launch_bounce_t<FIRST, HAS_BVH, 1024 + 158>(grid, in, out, b); break;
+        case 1024 + 186: launch_bounce_t<FIRST, HAS_BVH, 1024 + 186>(grid, in, out, b); break;
+        case 1024 + 190: launch_bounce_t<FIRST, HAS_BVH, 1024 + 190>(grid, in, out, b); break;
+#ifndef PT_VAR_PROBE
+        case 1024 + 530: launch_bounce_t<FIRST, HAS_BVH, 1024 + 530>(grid, in, out, b); break;
+        case 1024 + 562: launch_bounce_t<FIRST, HAS_BVH, 1024 + 562>(grid, in, out, b); break;
+        case 1024 + 666: launch_bounce_t<FIRST, HAS_BVH, 1024 + 666>(grid, in, out, b); break;
+        case 1024 + 698: launch_bounce_t<FIRST, HAS_BVH, 1024 + 698>(grid, in, out, b); break;
+#endif
         default: launch_bounce_t<FIRST, HAS_BVH, 3>(grid, in, out, b); break;   // unreachable: pt_init checks
     }
 }
+bool variant_compiled(int v);
 // the fused kernel's template variant for a bounce: the requested bits minus what this bounce /
 // scene does not use
 int effective_variant(bool first, int var, bool has_quads) {
@@ -1018,6 +1059,9 @@ int effective_variant(bool first, int var, bool has_quads) {
     if (first && skip_cam) var &= ~VAR_SECTION_TIMING;
     if (!g.split) var &= ~VAR_BVH_SPLIT;
     if (!has_quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
+    // the texture-free build exists for the default variants (and their section-counter and
+    // material-grouping forms); other variants keep the texture code
+    if (g.no_tex && variant_compiled(var | VAR_NO_TEX)) var |= VAR_NO_TEX;
     return var;
 }
 // variants instantiated in launch_bounce_v (pt_init refuses others instead of running a
@@ -1025,8 +1069,11 @@ int effective_variant(bool first, int var, bool has_quads) {
 bool variant_compiled(int v) {
     static const int k[] = {0, 1, 2, 6, 10, 18, 22, 26, 30, 50, 54, 58, 154, 158, 186, 190, 306, 310, 442, 446,
                             530, 562, 666, 698};
-    for (int x : k)
-        if (x == v) return true;
+    static const int kt[] = {18, 22, 50, 54, 154, 158, 186, 190, 530, 562, 666, 698};   // also with VAR_NO_TEX
+    const int* b = (v & VAR_NO_TEX) ? kt : k;
+    const int n = (v & VAR_NO_TEX) ? (int)(sizeof kt / sizeof kt[0]) : (int)(sizeof k / sizeof k[0]);
+    for (int i = 0; i < n; ++i)
+        if (b[i] == (v & ~VAR_NO_TEX)) return true;
     return false;
 }
 void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1062,7 +1109,8 @@ int tail_from(int batch) {
     const bool lds = g.sc.num_geoms <= LDS_GEOMS;
     static const bool any_batch = getenv("PT_TAIL_BATCH") && atoi(getenv("PT_TAIL_BATCH")) != 0;   // tools: A/B
     if (off || (batch != 1 && !any_batch) || g.has_bvh || !lds || depth < 3 ||
-        effective_variant(false, g.opts.variant, false) != (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
+        (effective_variant(false, g.opts.variant, false) & ~VAR_NO_TEX) !=
+            (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
         return 0;
     static const int from = getenv("PT_TAIL_FROM") ? atoi(getenv("PT_TAIL_FROM")) : 0;   // tools: A/B
     return std::min(depth - 1, std::max(1, from > 0 ? from : depth / 2));
@@ -1083,8 +1131,12 @@ int enqueue_pass_body(int batch) {
         if (t) {
             constexpr int V = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST;
             const size_t lds = sizeof(DevGeomHot) * g.sc.num_geoms + sizeof(BlockLds);
-            launch(300 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
-                   g.seg_stride, depth);
+            if (g.no_tex)
+                launch(300 + t, k_tail<V | VAR_NO_TEX>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl,
+                       g.d_image, t, g.seg_stride, depth);
+            else
+                launch(300 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
+                       g.seg_stride, depth);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
@@ -1631,6 +1683,10 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         d.bumpID = m.bumpID;
         d.bumpScale = m.bumpScale;
     }
+    // no material samples a texture or bump map: the fused kernels' texture-free build (VAR_NO_TEX)
+    g.no_tex = true;
+    for (int i = 0; i < s->num_materials; ++i)
+        if (s->materials[i].hasTexture || s->materials[i].hasBumpMap) g.no_tex = false;
     // BVH: only when the reference would traverse it (BVH_ACCELERATION and a non-empty tree)
     g.has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
     std::vector<DevNode> nodes;
