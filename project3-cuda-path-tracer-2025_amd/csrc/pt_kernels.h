@@ -1016,6 +1016,9 @@ PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) 
 #ifndef PT_DUP
 #define PT_DUP 0
 #endif
+#ifndef XSCAN_BALLOT
+#define XSCAN_BALLOT 1
+#endif
 PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
     const float4* rec = reinterpret_cast<const float4*>(sc.cull);
     const int ng = sc.num_geoms;
@@ -1287,6 +1290,18 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         sec_add(SEC_CULL, tc1 - tc0);
         sec_add_lanes(SEC_N_CAND, cnt);
     }
+#if XSCAN_BALLOT
+    // the wave's exclusive prefix sum of cnt, one bit plane at a time (ballot + mbcnt, no LDS
+    // round trips); a wave-uniform loop over the planes that are set somewhere (cornell: 2)
+    int wexcl = 0, wtot = 0;
+    for (int b = 0;; ++b) {
+        const uint64_t m = __ballot((cnt >> b) & 1);
+        wexcl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+        wtot += __popcll(m) << b;
+        if (!__any(cnt >> (b + 1))) break;
+    }
+    if (lane == 0) B->wsum[w] = wtot;
+#else
     int incl = cnt;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1294,6 +1309,8 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         if (lane >= off) incl += y;
     }
     if (lane == 63) B->wsum[w] = incl;
+    const int wexcl = incl - cnt;
+#endif
     __syncthreads();
     int woff = 0, total = 0;
 #pragma unroll
@@ -1302,7 +1319,7 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         woff += i < w ? x : 0;
         total += x;
     }
-    int excl = woff + incl - cnt;
+    int excl = woff + wexcl;
     // one register: left transparent, the compiler keeps the six scan partials and the four wave
     // sums live across the exact tests and re-adds them afterwards (10 VGPRs at the peak)
     asm volatile("" : "+v"(excl));
@@ -1335,7 +1352,11 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
     B->rd[2][tid] = rd.z;
     {
         int j = excl;
-        for (uint64_t m = cand; m; m &= m - 1) B->task[j++] = (uint16_t)((tid << 8) | __builtin_ctzll(m));
+        if (sc.num_geoms <= 32) {   // uniform: 32-bit mask arithmetic
+            for (uint32_t m = (uint32_t)cand; m; m &= m - 1) B->task[j++] = (uint16_t)((tid << 8) | __builtin_ctz(m));
+        } else {
+            for (uint64_t m = cand; m; m &= m - 1) B->task[j++] = (uint16_t)((tid << 8) | __builtin_ctzll(m));
+        }
     }
     __syncthreads();
     for (int k = w * 64 + lane; k < total; k += BLOCK) {
