@@ -393,12 +393,18 @@ PT_DEV f3 mulT(const M3& m, f3 v) {
               m.c2.x * v.x + m.c2.y * v.y + m.c2.z * v.z};
 }
 // coordinateSystem + LocalToWorld, interactions.h:14-27
+// Both branches as one sequence of the same operations (a wave whose lanes take different
+// branches ran both: 2 square roots and 6 divisions): the branch picks the operands, one sqrt and
+// two divisions follow, and the zero component 0 / s is +0 whenever s > 0 (s = +0 or NaN keeps
+// the division, so 0/0 and NaN propagate exactly as in the reference).
 PT_DEV M3 local_to_world(f3 n) {
-    f3 t;
-    if (__builtin_fabsf(n.x) > __builtin_fabsf(n.y))
-        t = mk(-n.z, 0, n.x) / __builtin_sqrtf(n.x * n.x + n.z * n.z);
-    else
-        t = mk(0, n.z, -n.y) / __builtin_sqrtf(n.y * n.y + n.z * n.z);
+    const bool xb = __builtin_fabsf(n.x) > __builtin_fabsf(n.y);
+    const float p = xb ? n.x : n.y;
+    const float s = __builtin_sqrtf(p * p + n.z * n.z);   // x: n.x n.x + n.z n.z; y: n.y n.y + n.z n.z
+    const float q1 = (xb ? -n.z : n.z) / s;                // x: t.x = -n.z / s;  y: t.y = n.z / s
+    const float q2 = (xb ? n.x : -n.y) / s;                // x: t.z = n.x / s;   y: t.z = -n.y / s
+    const float z = s > 0.0f ? 0.0f : 0.0f / s;
+    const f3 t = xb ? mk(q1, z, q2) : mk(z, q1, q2);
     return M3{t, cross(n, t), n};
 }
 
@@ -417,16 +423,15 @@ PT_DEV f3 hemisphere_cosine(float xi0, float xi1) {
     if (xi0 == 0.f && xi1 == 0.f) {
         x = 0.f; y = 0.f;
     } else {
-        float theta, radius;
+        // the two branches as one sequence (lanes of a wave take both at random: two divisions):
+        // the branch only picks the operands of the one division
         float a = (2.f * xi0) - 1.f;
         float b = (2.f * xi1) - 1.f;
-        if ((a * a) > (b * b)) {
-            radius = 1.f * a;
-            theta = PI_OVER_FOUR * (b / a);
-        } else {
-            radius = 1.f * b;
-            theta = PI_OVER_TWO - (PI_OVER_FOUR * (a / b));
-        }
+        const bool ab = (a * a) > (b * b);
+        const float radius = 1.f * (ab ? a : b);
+        const float r = (ab ? b : a) / (ab ? a : b);
+        const float qr = PI_OVER_FOUR * r;
+        const float theta = ab ? qr : PI_OVER_TWO - qr;
         float s, c;
         pt_sincosf(theta, &s, &c);
         x = radius * c;
