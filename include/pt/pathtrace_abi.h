@@ -85,8 +85,11 @@ typedef struct pt_options {
                                     that enter the mesh's root box are queued and traversed in
                                     full waves by a second kernel per bounce, 64: keep 16 on the
                                     reference node array instead of the paired-children layout,
-                                    128: with 8, the exact-test exchange spans the whole block);
-                                    results are bit-identical for every value.  Default
+                                    128: with 8, the exact-test exchange spans the whole block,
+                                    256: 4-wide BVH nodes, 512: material grouping, set by
+                                    material_sort; 1024 is set by pt_init itself when no material
+                                    has a texture or bump map: the kernels built without texel
+                                    fetches); results are bit-identical for every value.  Default
                                     2|8|16|32|128 */
     int32_t frames_per_pass;     /* pt_trace_frames traces F frames per wavefront pass (1..256;
                                     0 = auto: ~84M paths in flight, e.g. 128 at 800x800, 256 for

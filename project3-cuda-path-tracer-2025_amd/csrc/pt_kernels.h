@@ -63,6 +63,7 @@ struct SceneDev {
     const DevTriCold* cold;
     int num_geoms, num_mats, num_nodes, num_tris;
     int trace_depth, arg_order, use_bvh, stack_depth;
+    int pair_stack_depth;     // bvh_intersect_pairs' push bound (<= stack_depth)
     CamDev cam;
     ShardDev shard;
     float* contrib;     // passes of F > 1 frames: [slot][pixel] float3 of each terminated path
@@ -418,7 +419,7 @@ PT_DEV float cull_threshold_packed(float entry, float w) {
 // traversal state of one ray on the pair layout
 struct TravState {
     f3 ro, rd, rr;
-    float t_limit, t_hit, bu, bv;
+    float t_hit, bu, bv;   // t_hit starts at t_limit (the primitives' t): see trav_begin
     int btri, cur, sp;
     float curT;   // certified cull threshold of st.cur (0: none)
     bool exact;
@@ -433,8 +434,11 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
                      __builtin_fabsf(rd.z) < 0.00001f;
     st.wfast = __all(!(st.exact || par));
     st.rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-    st.t_limit = t_limit;
-    st.t_hit = FLT_MAX_;
+    // t_hit starts at the primitives' t_limit instead of FLT_MAX: the culls used min(t_hit,
+    // t_limit), which is then t_hit itself, and a triangle farther than t_limit can never win (the
+    // primitive keeps ties, make_hit's strict `<`), so the result is the same and the traversal
+    // carries one register fewer.  "No triangle" is btri still at its sentinel.
+    st.t_hit = t_limit;
     st.bu = st.bv = 0.f;
     st.btri = 0x7fffffff;
     st.sp = 0;
@@ -447,7 +451,7 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
 }
 // pop the nearest stack entry whose certified cull does not reject it (st.cur = -1: empty)
 PT_DEV void trav_pop(TravState& st, int* stack) {
-    const float tb = __builtin_fminf(st.t_hit, st.t_limit);
+    const float tb = st.t_hit;
     st.cur = -1;
     while (st.sp > 0) {
         const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
@@ -464,7 +468,7 @@ PT_DEV void trav_pop(TravState& st, int* stack) {
 // false: no child passes (the caller pops)
 template <bool COUNT = false>
 PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
-    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
+    const float t_best = st.t_hit;
     if (COUNT) n_nodes++;
     const DevPair pr = sc.pairs[st.cur];
 #ifdef PT_PROBE_EXTRA_LOAD   // tools: resource probe (one more dwordx4 gather per inner step, result unused)
@@ -506,7 +510,7 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
         st.curT = lfirst ? Tl : Tr;
         const int far = lfirst ? rrf : rl;
         const float Tf = lfirst ? Tr : Tl;
-        if (st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
+        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
         return true;
     }
     if (pl | pb) {
@@ -561,7 +565,7 @@ PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_node
 }
 // result of a finished traversal: t (-1: no triangle), u, v, hot4 slot (-1)
 PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
-    if (st.t_hit == FLT_MAX_) {
+    if (st.btri == 0x7fffffff) {
         btri = -1;
         return -1.f;
     }
@@ -576,7 +580,7 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
 template <bool COUNT = false>
 PT_DEV void trav_step_quad(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
     const int Q = sc.num_quads;
-    const float t_best = __builtin_fminf(st.t_hit, st.t_limit);
+    const float t_best = st.t_hit;
     const int cur = st.cur;
     bool next = false;
     if (cur < Q) {
@@ -647,7 +651,7 @@ PT_DEV void trav_step_quad(const SceneDev& sc, TravState& st, int* stack, int& n
         }
     }
     if (!next) {
-        const float tb = __builtin_fminf(st.t_hit, st.t_limit);
+        const float tb = st.t_hit;
         st.cur = -1;
         while (st.sp > 0) {
             const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
@@ -693,7 +697,7 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
         sec_add_lanes(SEC_N_NODES, n_nodes);
         sec_add_lanes(SEC_N_TRIS, n_tris);
         sec_add_lanes(SEC_N_BVH_RAYS, 1);
-        const bool hit = st.t_hit != FLT_MAX_ && st.t_hit < t_limit;   // the mesh changes the winner
+        const bool hit = st.btri != 0x7fffffff && st.t_hit < t_limit;   // the mesh changes the winner
         sec_add_lanes(SEC_N_BVH_HITS, hit ? 1 : 0);
         sec_add_lanes(SEC_N_MISS_NODES, hit ? 0 : n_nodes);
     }

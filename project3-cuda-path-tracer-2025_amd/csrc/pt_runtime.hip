@@ -865,6 +865,7 @@ struct State {
     int num_tex = 0;
     bool has_bvh = false;
     int stack_depth = 0;
+    int pair_depth = 0;              // entries the pair traversal needs: height of its hierarchy + 1
     size_t bvh_lds = 0;
     // device buffers
     DevGeom* d_geoms = nullptr;
@@ -993,7 +994,8 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), g.bvh_lds + lds_pad, g.sc, g.queue, out, g.d_ctl,
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
+               (size_t)g.sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, g.sc, g.queue, out, g.d_ctl,
                g.d_image, b, g.seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
@@ -1958,6 +1960,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         }
                     }
                     g.stack_depth = std::max(g.stack_depth, th + 1);
+                    g.pair_depth = th + 1;
                     if (getenv("PT_BVH_TREE_INFO"))
                         fprintf(stderr, "pt_init: SAH traversal tree over %d reference leaves, height %d (reference %d)\n", L,
                                 th, height);
@@ -2061,6 +2064,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         g.stack_depth = std::max(g.stack_depth, 3 * qh + 1);
                     }
                 }
+                if (!sah) g.pair_depth = height + 1;
                 pair_root_ref = sah ? 0 : ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
@@ -2180,6 +2184,11 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.arg_order = o.arg_order;
     sc.use_bvh = g.has_bvh ? 1 : 0;
     sc.stack_depth = g.stack_depth;
+    // the pair traversal pushes at most one entry per level of its hierarchy (never more than the
+    // stack_depth the other traversals size their stacks for); k_bvh_bounce's LDS stack is sized
+    // by it -- unless k_bvh_bounce walks the 4-wide layout, which needs stack_depth
+    sc.pair_stack_depth = g.pair_depth > 0 ? std::min(g.pair_depth, g.stack_depth) : g.stack_depth;
+    if (g.d_quads) sc.pair_stack_depth = g.stack_depth;
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
     sc.contrib = g.d_contrib;
