@@ -308,7 +308,9 @@ def sub_config(ptamd, cfg):
            "segments_per_frame": round(st["segments_total"] / steps, 1), "frames_per_pass": st["frames_per_pass"],
            "data": "synthetic stand-in meshes (reference OBJs absent)" if "obj" in scene_name else "reference scene",
            "roofline": roofline(prof, st_prof, pipeline, steps, d, False,
-                                traffic_file="c4_bunny" if "bnnuy" in scene_name and res is None else None),
+                                traffic_file=("c4_bunny" if "bnnuy" in scene_name and res is None else
+                                              "c5_khaslana" if "khaslana" in scene_name and res == (1600, 1600)
+                                              and depth == 12 else None)),
            "kernels": kernels_digest(prof, None)}
     if tag == "configs[4]":
         out["note"] = "BASELINE names 8 GPUs for this config; this sub-record is one GPU (bench.py --gpus 8 --scene ...)"
