@@ -434,6 +434,13 @@ PT_DEV f3 hemisphere_cosine(float xi0, float xi1) {
         const float theta = ab ? qr : PI_OVER_TWO - qr;
         float s, c;
         pt_sincosf(theta, &s, &c);
+#if PT_DUP == 5   // tools: the sincos's cost, counted twice (result discarded)
+        {
+            float s2, c2;
+            pt_sincosf(theta + 0.0f * xi1, &s2, &c2);
+            asm volatile("" ::"v"(s2), "v"(c2));
+        }
+#endif
         x = radius * c;
         y = radius * s;
     }
