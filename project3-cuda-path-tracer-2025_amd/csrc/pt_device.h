@@ -154,9 +154,9 @@ struct DevCull {
 };
 static_assert(sizeof(DevCull) == 48, "DevCull");
 
-// geom_test's cube early-out, on ONE object axis a, with geom_test's own arithmetic for qo[a]
-// and u[a] (xform row a).  True only when geom_test would return -1 through that early-out: the
-// object-space origin is outside slab a and the direction points away.  u[a]'s w term
+// The "away" case of geom_test's cube (see the comment there), on ONE object axis a, with
+// geom_test's own arithmetic for qo[a] and u[a] (xform row a).  True only when geom_test's slab
+// test certainly returns -1: the object-space origin is outside slab a and the direction points away.  u[a]'s w term
 // (m[9 + a] * 0 = +-0) is left out: it cannot change a nonzero u[a], and `u > 0` / `u < 0` are
 // false for either zero.  geom_test also requires dot(u, u) < inf; the caller guarantees it
 // (|rd| components <= 1e3 and |inv| entries <= 1e12, checked on the host).
@@ -278,17 +278,14 @@ PT_DEV float geom_test(const DevGeomHot& g, f3 ro, f3 rd, f3& seed) {
     const f3 qo = xform(g.inv, ro, 1.0f);
     const f3 u = xform(g.inv, rd, 0.0f);
     const float uu = dot(u, u);
-    if (g.type == PT_CUBE) {
-        // Early out that cannot change the result: on an axis where the object-space origin is
-        // outside the slab and the direction points away (qo > .5, u > 0 or qo < -.5, u < 0),
-        // both slab distances below are negative (|0.5 - qo| >= 2^-24, |qd| <= 1), so tmax < 0
-        // and the reference's test reports a miss.  sign(qd) = sign(u) because qd = u * s with
-        // s = 1/sqrt(uu) > 0 finite (uu < inf; u == +-0 underflow still gives -inf distances).
-        const bool away = (qo.x > 0.5f && u.x > 0.0f) || (qo.x < -0.5f && u.x < 0.0f) ||
-                          (qo.y > 0.5f && u.y > 0.0f) || (qo.y < -0.5f && u.y < 0.0f) ||
-                          (qo.z > 0.5f && u.z > 0.0f) || (qo.z < -0.5f && u.z < 0.0f);
-        if (away && uu < __builtin_inff()) return -1.0f;
-    }
+    // A cube the ray leaves on some axis (object-space origin outside the slab, direction pointing
+    // away: qo > .5, u > 0 or qo < -.5, u < 0) is always a miss below: both slab distances on
+    // that axis are negative (|0.5 - qo| >= 2^-24, |qd| <= 1), so tmax < 0.  sign(qd) = sign(u)
+    // because qd = u * s with s = 1/sqrt(uu) > 0 finite (uu < inf; u == +-0 underflow still gives
+    // -inf distances).  The pre-test's away row (away_on_axis) drops such candidates on that
+    // argument.  Round 2 also returned early here on it; the exact tests now see few such cubes
+    // and the check's ~12 instructions per test cost more than the skipped tests: cornell -2.1 %,
+    // khaslana -0.8 % without it (A/B, round 3), same bits.
     const f3 qd = u * (1.0f / __builtin_sqrtf(uu));      // normalize(u), func_geometric.inl:158
     bool hit;
     float tq;
@@ -448,6 +445,17 @@ PT_DEV f3 hemisphere_cosine(float xi0, float xi1) {
     return mk(x, y, z);
 }
 
+// x / PI correctly rounded, for x = 0 or x in [2^-24, 1] -- the cosine sample's z (the square root
+// of (1 - x^2) - y^2 with x, y in [-1, 1]: 0 or at least 2^-24): one product with RN(1 / PI) and
+// one residual correction (Markstein), 3 operations instead of the division's ~10 with a
+// quarter-rate reciprocal.  tools/check_div_by_pi.c checks it against IEEE division for every
+// float from 0 to 1 (and every non-negative normal float): identical bits; tests/test_libm.py runs it.
+PT_DEV float div_by_pi(float x) {
+    const float INV_PI_RN = 0.318309873342514038085938f;   // RN(1 / PI) = 0x1.45f306p-2
+    const float q = x * INV_PI_RN;
+    const float r = __builtin_fmaf(-PI, q, x);
+    return __builtin_fmaf(r, INV_PI_RN, q);
+}
 // sampleFDiffuse, interactions.cu:92-108 (returns bsdf; pdf, wiW out)
 PT_DEV f3 sample_diffuse(f3 albedo, f3 normal, f3& wiW, float& pdf, Rng& rng, int arg_order) {
     float xi0, xi1;
@@ -455,7 +463,7 @@ PT_DEV f3 sample_diffuse(f3 albedo, f3 normal, f3& wiW, float& pdf, Rng& rng, in
     f3 wi = hemisphere_cosine(xi0, xi1);
     M3 ws = local_to_world(normal);
     wiW = normalize_unit(mul(ws, wi));
-    pdf = wi.z / PI;
+    pdf = div_by_pi(wi.z);
     return albedo * INV_PI;
 }
 

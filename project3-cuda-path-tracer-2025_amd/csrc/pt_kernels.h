@@ -998,7 +998,7 @@ PT_DEV void tex_fetch(const SceneDev& sc, int id, float x, float y, float out[4]
 // the reference's `t > 0 && t_min > t` rule, so the winner (first minimum) is unchanged.  Every
 // lane of the wave must call this (uniform control flow); `live` = the lane has a ray.
 // candidates the exchanged exact test would certainly reject: a cube the ray leaves through
-// geom_test's own "away" early-out (away_on_axis).  `bounded`: |rd| components <= 1e3
+// on an axis while pointing away from it, which geom_test's slab test always rejects (away_on_axis).  `bounded`: |rd| components <= 1e3
 // (away_on_axis' precondition).  Spheres keep theirs: most sphere candidates are rays leaving
 // the sphere, whose exact test can round to a self-hit at t ~ 1e-4 (t1 = -b + sqrt(b^2 - ~0) =
 // 0), so only the reference arithmetic can reject them (a bounding-ball line test dropped 3 % of
@@ -1077,8 +1077,8 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, 
     if (live) {
         cr = cull_ray(ro, rd);
         // a ray leaving a surface keeps that surface's box as a candidate (its origin sits inside
-        // the margin), but geom_test's "away" early-out rejects it: drop such candidates here,
-        // with the same arithmetic, so they take no slot in the exchanged exact tests
+        // the margin), but geom_test's slab test rejects it ("away", see geom_test): drop such
+        // candidates here, with the same arithmetic, so they take no slot in the exact tests
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
         cand = cull_candidates(sc, cr, ro, rd, bounded);
