@@ -267,6 +267,32 @@ PT_DEV float u01(Rng& r) { return (float)(rng_next(r) - 1u) * 4.6566128730773925
 // getPointOnRay, intersections.h:29-32
 PT_DEV f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize_unit(d); }   // d: unit q.direction
 
+// The slab distances' two divisions per axis share one divisor.  AMDGPU's IEEE float division is
+// div_scale(b), div_scale(a), y = rcp(b) refined by one Newton step, q = a * y corrected twice by
+// its residual (the second through div_fmas), then div_fixup.  Where neither div_scale scales nor
+// div_fixup replaces the result, that is exactly div_rcp + div_with_rcp below, so the refined
+// reciprocal can be computed once per axis: 3 + 2 x 5 operations instead of 2 x 10, and one
+// quarter-rate rcp instead of two.  slab_div_ok certifies that range for all three axes:
+// |qd| >= 2^-40 (no zero, denormal or huge-reciprocal divisor) and |qo| <= 2^40, so the numerators
+// (+-0.5 - qo) are 0 or of magnitude >= 2^-25 (exact Sterbenz differences near +-0.5) and at most
+// 2^40 + 0.5: the exponent gap stays below div_scale's 96, no quotient, reciprocal or residual
+// leaves the normal range, and a zero numerator gives the IEEE zero (sign of qd) without the
+// fixup.  Anything else (axis-aligned or NaN directions, far origins) takes the division.
+PT_DEV bool slab_div_ok(f3 qo, f3 qd) {
+    const float dmin = fminf(fminf(__builtin_fabsf(qd.x), __builtin_fabsf(qd.y)), __builtin_fabsf(qd.z));
+    const float omax = fmaxf(fmaxf(__builtin_fabsf(qo.x), __builtin_fabsf(qo.y)), __builtin_fabsf(qo.z));
+    return dmin >= 0x1p-40f && omax <= 0x1p40f;
+}   // (fminf / fmaxf skip a NaN component; its distances are NaN either way, and only compared)
+PT_DEV float div_rcp(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+PT_DEV float div_with_rcp(float a, float b, float y) {
+    const float q0 = a * y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
+}
+
 // boxIntersectionTest (intersections.cu:3-57) and sphereIntersectionTest (intersections.cu:
 // 59-109) as ONE routine: both start by taking the ray to object space (q.origin, normalized
 // q.direction) and end with the world hit point's distance, so a wave whose lanes test a mix of
@@ -296,11 +322,19 @@ PT_DEV float geom_test(const DevGeomHot& g, f3 ro, f3 rd, f3& seed) {
         // as a code (axis + 1) * sign, decoded to the same bits at the end -- 2 registers, not 6, at
         // the fused kernel's peak register pressure (this runs inside the exact-test exchange)
         int tmin_c = 0, tmax_c = 0;
+        const bool shared_rcp = slab_div_ok(qo, qd);
 #pragma unroll
         for (int xyz = 0; xyz < 3; ++xyz) {
             float qdx = comp(qd, xyz), qox = comp(qo, xyz);
-            float t1 = (-0.5f - qox) / qdx;
-            float t2 = (+0.5f - qox) / qdx;
+            float t1, t2;
+            if (shared_rcp) {
+                const float y = div_rcp(qdx);
+                t1 = div_with_rcp(-0.5f - qox, qdx, y);
+                t2 = div_with_rcp(+0.5f - qox, qdx, y);
+            } else {
+                t1 = (-0.5f - qox) / qdx;
+                t2 = (+0.5f - qox) / qdx;
+            }
             float ta = gmin(t1, t2);
             float tb = gmax(t1, t2);
             const int nc = t2 < t1 ? xyz + 1 : -(xyz + 1);

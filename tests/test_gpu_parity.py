@@ -69,6 +69,10 @@ def _random_paths(n, seed, box=5.0):
     # axis-aligned and degenerate directions exercise the slab tests' inf / NaN paths
     d[: n // 16] = np.eye(3, dtype=np.float32)[np.arange(n // 16) % 3] * np.where(np.arange(n // 16) % 2, 1, -1)[:, None]
     d[n // 16: n // 16 + 4] = np.nan
+    # components around geom_test's shared-reciprocal bound (|qd| >= 2^-40 in object space)
+    k = np.arange(24)
+    tiny = np.ldexp(np.where(k % 2, -1.0, 1.0) * (1 + (k % 3 - 1) * 2.0 ** -23), -34 - k // 2)
+    d[n // 16 + 4: n // 16 + 28] = np.stack([np.full(24, 0.6), tiny, np.full(24, -0.8)], 1)
     p["direction"] = d
     p["color"] = rng.uniform(0.1, 1.0, (n, 3)).astype(np.float32)
     p["pixelIndex"] = rng.integers(0, 640000, n)
