@@ -1650,8 +1650,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             }
         }
     }
-    // padded to a multiple of 4 records (cull_candidates reads 4 at a time; pad bits are masked)
-    std::vector<DevCull> culls((std::max(1, s->num_geoms) + 3) & ~3);
+    // padded to a multiple of CULL_GROUP records (cull_candidates reads that many at a time; pad
+    // bits are masked)
+    std::vector<DevCull> culls((std::max(1, s->num_geoms) + CULL_GROUP - 1) / CULL_GROUP * CULL_GROUP);
     for (DevCull& c : culls) memset(&c, 0, sizeof c);
     for (int i = 0; i < s->num_geoms; ++i) {
         const DevGeom& d = geoms[i];
