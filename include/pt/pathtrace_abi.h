@@ -13,7 +13,10 @@
  * include/pathtrace.h keeps the reference's exact void signatures on top of this ABI.
  *
  * State is process-global like the reference's file-static device buffers
- * (pathtrace.cu:82-101); the library is not re-entrant.  All arrays are in the reference's
+ * (pathtrace.cu:82-101); the library is not re-entrant.  One process may drive several GPUs:
+ * pt_options.num_devices > 1 splits every frame into pixel shards, one per device, traced
+ * concurrently and combined into the first device's image after every pt_trace / pt_trace_frames
+ * call (over xGMI peer access or RCCL) -- the same pathtrace() call, the same image, bit for bit.  All arrays are in the reference's
  * own layouts (include/pt/scene_structs.h); the library converts them once, at pt_init, to
  * its device layout.  Every function returns PT_OK (0) or a negative PT_E* code;
  * pt_last_error() gives the message.
@@ -30,7 +33,10 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+/* 2: pt_options gained num_devices / device_ids / combine, pt_frame_stats queued_total,
+ *    pt_kernel_times tail_ms / tail_from; pt_set_trace_depth */
+#define PT_ABI_VERSION 2
+#define PT_MAX_DEVICES 16
 
 enum {
     PT_OK = 0,
@@ -57,6 +63,7 @@ typedef struct pt_scene_view {
 
 enum { PT_PIPELINE_FUSED = 0, PT_PIPELINE_STAGED = 1 };
 enum { PT_SHARD_NONE = 0, PT_SHARD_PIXELS = 1, PT_SHARD_SAMPLES = 2 };
+enum { PT_COMBINE_PEER = 0, PT_COMBINE_RCCL = 1 };
 
 typedef struct pt_options {
     int32_t stream_compaction;   /* STREAM_COMPACTION (pathtrace.cu:21), default 1 */
@@ -96,6 +103,19 @@ typedef struct pt_options {
                                     a 1/8 pixel shard of it).  The image is bit-identical
                                     to frame-by-frame tracing: terminated paths of a pass land in
                                     per-frame planes that are added in frame order. */
+    /* ---- ABI 2: several GPUs behind one pathtrace() ---- */
+    int32_t num_devices;         /* 0 or 1: one device (`device`).  N > 1: N shard contexts; shard k traces the
+                                    interleaved row bands (y / shard_rows) % N == k on device device_ids[k]
+                                    (entries may repeat: shards on one GPU run on their own streams).
+                                    Requires shard_mode == PT_SHARD_NONE (this is the in-process form of
+                                    PT_SHARD_PIXELS).  pt_default_options reads PT_DEVICES from the
+                                    environment: "N" (devices 0..N-1) or a list "0,1,1" */
+    int32_t device_ids[PT_MAX_DEVICES];   /* default k -> k */
+    int32_t combine;             /* how shard images reach the first device's image: PT_COMBINE_PEER (default:
+                                    a kernel on the first device reads each shard's pixels over xGMI peer
+                                    access) or PT_COMBINE_RCCL (each shard packs its pixels, one RCCL group of
+                                    send / recv over a communicator of the distinct devices, librccl.so loaded
+                                    at pt_init).  Environment default: PT_COMBINE=rccl|peer */
 } pt_options;
 
 typedef struct pt_frame_stats {
@@ -165,6 +185,9 @@ int32_t pt_reset_stats(void);
 
 /* Camera update without re-upload (main.cpp:423-444 path); resets nothing else. */
 int32_t pt_set_camera(const pt_camera* camera);
+/* RenderState::traceDepth, re-read by the reference at every pathtrace() call (pathtrace.cu:641):
+ * the depth of the next frames (0 .. 64); resets nothing else. */
+int32_t pt_set_trace_depth(int32_t depth);
 
 /* ---- scene ingest (C++ restatement of scene.cpp, host/scene.cpp) for non-C++ callers ---- */
 typedef struct pt_scene_file pt_scene_file;

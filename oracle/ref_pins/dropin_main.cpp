@@ -8,18 +8,23 @@
 // pathtrace(pbo, 0, iteration) per frame, pathtraceFree at the end — minus GLFW / ImGui / the GL
 // PBO (pbo = NULL, the headless case the drop-in accepts).
 //
-//   dropin_main <scene.json> <frames> <out.f32>   -> writes scene->state.image after the last
-//                                                    frame and prints "traced_depth <n>"
+//   dropin_main <scene.json> <frames> <out.f32> [F:D]  -> writes scene->state.image after the last
+//                                                    frame and prints "traced_depth <n>"; with F:D
+//                                                    the caller sets state.traceDepth = D before
+//                                                    frame F (the reference re-reads it per frame,
+//                                                    pathtrace.cu:641)
 #include "pathtrace.h"
 
 #include <cstdio>
 #include <cstdlib>
 
 int main(int argc, char** argv) {
-    if (argc != 4) {
-        std::printf("Usage: %s SCENEFILE.json FRAMES OUT.f32\n", argv[0]);
+    if (argc != 4 && argc != 5) {
+        std::printf("Usage: %s SCENEFILE.json FRAMES OUT.f32 [FRAME:DEPTH]\n", argv[0]);
         return 1;
     }
+    int depth_frame = -1, depth_value = 0;
+    if (argc == 5 && std::sscanf(argv[4], "%d:%d", &depth_frame, &depth_value) != 2) return 1;
     Scene* scene = new Scene(argv[1]);
     GuiDataContainer* guiData = new GuiDataContainer();
     RenderState* renderState = &scene->state;
@@ -72,6 +77,7 @@ int main(int argc, char** argv) {
         if (iteration < frames) {
             uchar4* pbo_dptr = NULL;
             iteration++;
+            if (iteration == depth_frame) renderState->traceDepth = depth_value;
             pathtrace(pbo_dptr, 0, iteration);
         } else {
             break;

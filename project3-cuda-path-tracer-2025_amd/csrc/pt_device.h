@@ -24,6 +24,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));   // native vector: one d
 
 #define PT_DEV __device__ __forceinline__
 
+// Measurement hooks: nothing in the product.  Tool builds (-DPT_TOOLS -I../tools) take their
+// definitions from tools/pt_tool_hooks.h (section duplicates for VALU attribution, resource probes).
+#ifdef PT_TOOLS
+#include "pt_tool_hooks.h"
+#else
+#define PT_HOOK(...) ((void)0)
+#endif
+
 namespace ptd {
 
 // utilities.h:13-20
@@ -465,13 +473,7 @@ PT_DEV f3 hemisphere_cosine(float xi0, float xi1) {
         const float theta = ab ? qr : PI_OVER_TWO - qr;
         float s, c;
         pt_sincosf(theta, &s, &c);
-#if PT_DUP == 5   // tools: the sincos's cost, counted twice (result discarded)
-        {
-            float s2, c2;
-            pt_sincosf(theta + 0.0f * xi1, &s2, &c2);
-            asm volatile("" ::"v"(s2), "v"(c2));
-        }
-#endif
+        PT_HOOK(DUP_SINCOS, theta, xi1);
         x = radius * c;
         y = radius * s;
     }

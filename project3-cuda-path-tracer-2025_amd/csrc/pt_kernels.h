@@ -139,14 +139,14 @@ PT_DEV void store_path(const PathBuf& b, int i, const PathReg& p) {
 }
 
 // local path id of this process -> global pixel index (PIXELS shard: interleaved row bands)
-PT_DEV int shard_pixel(const SceneDev& sc, int l) {
-    if (sc.shard.mode != 1) return l;
-    int W = sc.cam.resx;
+PT_DEV int shard_pixel_of(const ShardDev& sh, int W, int l) {
+    if (sh.mode != 1) return l;
     int lr = l / W, x = l - lr * W;
-    int band = lr / sc.shard.rows, within = lr - band * sc.shard.rows;
-    int y = (band * sc.shard.count + sc.shard.rank) * sc.shard.rows + within;
+    int band = lr / sh.rows, within = lr - band * sh.rows;
+    int y = (band * sh.count + sh.rank) * sh.rows + within;
     return x + y * W;
 }
+PT_DEV int shard_pixel(const SceneDev& sc, int l) { return shard_pixel_of(sc.shard, sc.cam.resx, l); }
 
 // generateRayFromCamera + sampleAperture (pathtrace.cu:231-292) for pixel `index`
 PT_DEV PathReg camera_ray(const CamDev& cam, int iter, int trace_depth, int index) {
@@ -471,20 +471,7 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
     const float t_best = st.t_hit;
     if (COUNT) n_nodes++;
     const DevPair pr = sc.pairs[st.cur];
-#ifdef PT_PROBE_EXTRA_LOAD   // tools: resource probe (one more dwordx4 gather per inner step, result unused)
-    {
-        const v4f x = reinterpret_cast<const v4f*>(sc.pairs)[4 * (size_t)(st.cur ^ 1) + 1];
-        asm volatile("" ::"v"(x[0]));
-    }
-#endif
-#ifdef PT_PROBE_EXTRA_VALU   // tools: resource probe (PT_PROBE_EXTRA_VALU dependent VALU per inner step)
-    {
-        float y = pr.l_lo.x;
-#pragma unroll
-        for (int k = 0; k < PT_PROBE_EXTRA_VALU; ++k) asm volatile("v_add_f32 %0, %0, %0" : "+v"(y));
-        asm volatile("" ::"v"(y));
-    }
-#endif
+    PT_HOOK(PROBE_INNER, sc, st.cur, pr);
     float el = 0.f, er = 0.f;
     bool pl, pb;
     if (st.wfast) {   // wave-uniform
@@ -1017,9 +1004,6 @@ PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) 
 #ifndef CULL_GROUP
 #define CULL_GROUP 4
 #endif
-#ifndef PT_DUP
-#define PT_DUP 0
-#endif
 #ifndef XSCAN_BALLOT
 #define XSCAN_BALLOT 1
 #endif
@@ -1279,13 +1263,7 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
         cand = cull_candidates(sc, cr, ro, rd, bounded);
-#if PT_DUP == 1   // tools/valu_attrib.sh: the section's VALU counted twice (result discarded)
-        {
-            const f3 ro2 = ro + mk(0.f, 0.f, 0.f);
-            const uint64_t c2 = cull_candidates(sc, cull_ray(ro2, rd), ro2, rd, bounded);
-            asm volatile("" ::"v"((uint32_t)c2), "v"((uint32_t)(c2 >> 32)));
-        }
-#endif
+        PT_HOOK(DUP_CULL, sc, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);
     uint64_t tc1 = 0;
@@ -1370,13 +1348,7 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         const f3 d = mk(B->rd[0][src], B->rd[1][src], B->rd[2][src]);
         f3 s;
         const float t = geom_test(lg[gi], o, d, s);
-#if PT_DUP == 2
-        {
-            f3 s2;
-            const float t2 = geom_test(lg[gi], o + mk(0.f, 0.f, 0.f), d, s2);
-            asm volatile("" ::"v"(t2), "v"(s2.x), "v"(s2.y), "v"(s2.z));
-        }
-#endif
+        PT_HOOK(DUP_EXACT, lg[gi], o, d);
         B->rt[k] = t;
         B->rs[0][k] = s.x;
         B->rs[1][k] = s.y;

@@ -18,8 +18,10 @@
 //
 // A frame is captured once into a hipGraph and replayed; the iteration number lives in
 // device memory (k_frame_begin advances it), so the replay needs no parameter updates.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <rccl/rccl.h>   // types only: librccl.so is opened at run time (PT_COMBINE_RCCL)
 
 #include <algorithm>
 #include <cmath>
@@ -109,6 +111,38 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
     px[0] = r;
     px[1] = gch;
     px[2] = b;
+}
+
+// Multi-device combine (pt_options.num_devices > 1): shard k owns the pixels
+// shard_pixel_of(sh_k, W, l), l < sh_k.local_pixels, of every shard image; the first device's
+// image receives them after each call.  Plain copies: the image is bit-identical to one device's.
+__global__ __launch_bounds__(BLOCK) void k_pull_shard(float* __restrict__ image, ShardDev sh, int W,
+                                                      const float* __restrict__ src) {   // src: a peer's image
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= sh.local_pixels) return;
+    const size_t pix = 3 * (size_t)shard_pixel_of(sh, W, l);
+    const float r = src[pix], gch = src[pix + 1], b = src[pix + 2];
+    image[pix] = r;
+    image[pix + 1] = gch;
+    image[pix + 2] = b;
+}
+__global__ __launch_bounds__(BLOCK) void k_pack_tile(const float* __restrict__ image, ShardDev sh, int W,
+                                                     float* __restrict__ tile) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= sh.local_pixels) return;
+    const size_t pix = 3 * (size_t)shard_pixel_of(sh, W, l);
+    tile[3 * (size_t)l] = image[pix];
+    tile[3 * (size_t)l + 1] = image[pix + 1];
+    tile[3 * (size_t)l + 2] = image[pix + 2];
+}
+__global__ __launch_bounds__(BLOCK) void k_unpack_tile(float* __restrict__ image, ShardDev sh, int W,
+                                                       const float* __restrict__ tile) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= sh.local_pixels) return;
+    const size_t pix = 3 * (size_t)shard_pixel_of(sh, W, l);
+    image[pix] = tile[3 * (size_t)l];
+    image[pix + 1] = tile[3 * (size_t)l + 1];
+    image[pix + 2] = tile[3 * (size_t)l + 2];
 }
 
 // --------------------------------------------------------------------------------------------
@@ -258,27 +292,14 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             if (!queued) h = finish_hit<false>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else if (REDIST && lds_geoms) {
             h = finish_hit<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid, qt, qw, qs);
-#if PT_DUP == 4
-            {
-                const Hit h2 = finish_hit<HAS_BVH, BVH_FAST>(sc, p.o, p.d + mk(0.f, 0.f, 0.f), s_stack + tid, qt, qw, qs);
-                asm volatile("" ::"v"(h2.t), "v"(h2.n.x), "v"(h2.n.y), "v"(h2.n.z), "v"(h2.mat));
-            }
-#endif
+            PT_HOOK(DUP_HIT, HAS_BVH, BVH_FAST, sc, p.o, p.d, s_stack + tid, qt, qw, qs);
         } else {
             h = lds_geoms ? intersect_scene_q<HAS_BVH, TIMING, BVH_FAST, FIRST>(sc, s_geoms, p.o, p.d, s_stack + tid)
                           : intersect_scene<HAS_BVH, BVH_FAST>(sc, p.o, p.d, s_stack + tid);
         }
         if (!MG && !queued) {
             uint64_t ts = TIMING ? sec_clock() : 0;
-#if PT_DUP == 3
-            {
-                PathReg q = p;
-                q.c = q.c + mk(0.f, 0.f, 0.f);
-                shade_path<(VAR & VAR_NO_TEX) == 0>(sc, q, h, iter + q.slot, [&]() { return hit_attr(sc, h); });
-                asm volatile("" ::"v"(q.c.x), "v"(q.c.y), "v"(q.c.z), "v"(q.d.x), "v"(q.d.y), "v"(q.d.z), "v"(q.o.x),
-                             "v"(q.o.y), "v"(q.o.z), "v"(q.rb));
-            }
-#endif
+            PT_HOOK(DUP_SHADE, (VAR & VAR_NO_TEX) == 0, sc, p, h, iter);
             shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
             if (TIMING) {
                 tc = sec_clock();
@@ -908,23 +929,24 @@ struct State {
     int32_t* traced_depth = nullptr;
     int key_bits = 1;
 };
-State g;
+State g_primary;                 // the process's context (shard 0 of a multi-device context)
+State* gp = &g_primary;          // the context the host runtime works on now (see ShardScope)
 int ensure_frames(int frames);
 
 // Host <-> device copies and memsets of the runtime, ordered on the library's stream and
-// completed before returning.  g.stream is a non-blocking stream: the legacy null stream that
+// completed before returning.  gp->stream is a non-blocking stream: the legacy null stream that
 // plain hipMemset / hipMemcpy use does not order against it, so a memset of FrameCtl could land
-// after a kernel enqueued behind it on g.stream (pt_test_camera saw a zeroed path count).
+// after a kernel enqueued behind it on gp->stream (pt_test_camera saw a zeroed path count).
 hipError_t smemset(void* p, int v, size_t n) {
-    hipError_t e = hipMemsetAsync(p, v, n, g.stream);
-    return e != hipSuccess ? e : hipStreamSynchronize(g.stream);
+    hipError_t e = hipMemsetAsync(p, v, n, gp->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(gp->stream);
 }
 hipError_t smemcpy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
-    hipError_t e = hipMemcpyAsync(dst, src, n, kind, g.stream);
-    return e != hipSuccess ? e : hipStreamSynchronize(g.stream);
+    hipError_t e = hipMemcpyAsync(dst, src, n, kind, gp->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(gp->stream);
 }
 
-PathBuf pathbuf(int i) { return PathBuf{g.d_path[i][0], g.d_path[i][1], g.d_path[i][2]}; }
+PathBuf pathbuf(int i) { return PathBuf{gp->d_path[i][0], gp->d_path[i][1], gp->d_path[i][2]}; }
 
 // pt_profile_frames: every kernel of the frame is launched with hipExtLaunchKernel's start/stop
 // events, which take their timestamps from that dispatch packet itself -- the kernel's own
@@ -959,46 +981,46 @@ template <class K, class... A>
 void launch(int kind, K kernel, dim3 grid, dim3 block, uint32_t lds, A... args) {
     if (g_prof) {
         ProfRec r{kind, prof_event(), prof_event()};
-        hipExtLaunchKernelGGL(kernel, grid, block, lds, g.stream, r.start, r.stop, 0, args...);
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, gp->stream, r.start, r.stop, 0, args...);
         g_prof->push_back(r);
     } else {
-        hipLaunchKernelGGL(kernel, grid, block, lds, g.stream, args...);
+        hipLaunchKernelGGL(kernel, grid, block, lds, gp->stream, args...);
     }
 }
 int nblocks(int n) { return (n + BLOCK - 1) / BLOCK; }
 
 void release_graph() {
     for (int f = 0; f <= MAXF; ++f) {
-        if (g.graph_exec[f]) (void)hipGraphExecDestroy(g.graph_exec[f]);
-        if (g.graph[f]) (void)hipGraphDestroy(g.graph[f]);
-        g.graph_exec[f] = nullptr;
-        g.graph[f] = nullptr;
+        if (gp->graph_exec[f]) (void)hipGraphExecDestroy(gp->graph_exec[f]);
+        if (gp->graph[f]) (void)hipGraphDestroy(gp->graph[f]);
+        gp->graph_exec[f] = nullptr;
+        gp->graph[f] = nullptr;
     }
 }
 
 // device-side counter of the input of bounce b in the staged pipeline
-const int* staged_count(int b) { return &g.d_ctl->cnt[b][0][0]; }
+const int* staged_count(int b) { return &gp->d_ctl->cnt[b][0][0]; }
 
 template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
-    const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && g.sc.num_geoms <= LDS_GEOMS;
-    const size_t geom_lds = lds ? sizeof(DevGeomHot) * g.sc.num_geoms : 0;
+    const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && gp->sc.num_geoms <= LDS_GEOMS;
+    const size_t geom_lds = lds ? sizeof(DevGeomHot) * gp->sc.num_geoms : 0;
     // the exchange's region: block_intersect's BlockLds, or one WaveLds per wave (wave_intersect)
     const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds
                                   ? ((VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : sizeof(WaveLds) * (BLOCK / 64))
                                   : 0;
-    const size_t stack_lds = HAS_BVH && !SPLIT ? g.bvh_lds : 0;
+    const size_t stack_lds = HAS_BVH && !SPLIT ? gp->bvh_lds : 0;
     // VAR_MAT_GROUP's exchange reuses the exact-test exchange's region (it runs after it)
     const size_t xchg_lds = (VAR & VAR_MAT_GROUP) ? std::max(redist_lds, mat_group_lds(HAS_BVH, false)) : redist_lds;
-    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds, g.sc, in, out,
-           g.d_ctl, g.d_image, b, g.seg_stride, g.queue);
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds, gp->sc, in, out,
+           gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
         launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
-               (size_t)g.sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, g.sc, g.queue, out, g.d_ctl,
-               g.d_image, b, g.seg_stride);
+               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, out, gp->d_ctl,
+               gp->d_image, b, gp->seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1061,11 +1083,11 @@ int effective_variant(bool first, int var, bool has_quads) {
     // tools: PT_SECTIONS_SKIP_CAMERA=1 leaves the camera bounce out of the section counters
     static const bool skip_cam = getenv("PT_SECTIONS_SKIP_CAMERA") != nullptr;
     if (first && skip_cam) var &= ~VAR_SECTION_TIMING;
-    if (!g.split) var &= ~VAR_BVH_SPLIT;
+    if (!gp->split) var &= ~VAR_BVH_SPLIT;
     if (!has_quads || !(var & VAR_BVH_SPLIT)) var &= ~VAR_BVH_QUAD;
     // the texture-free build exists for the default variants (and their section-counter and
     // material-grouping forms); other variants keep the texture code
-    if (g.no_tex && variant_compiled(var | VAR_NO_TEX)) var |= VAR_NO_TEX;
+    if (gp->no_tex && variant_compiled(var | VAR_NO_TEX)) var |= VAR_NO_TEX;
     return var;
 }
 // variants instantiated in launch_bounce_v (pt_init refuses others instead of running a
@@ -1081,7 +1103,7 @@ bool variant_compiled(int v) {
     return false;
 }
 void launch_bounce(bool first, bool bvh, int var, dim3 grid, PathBuf in, PathBuf out, int b) {
-    var = effective_variant(first, var, g.sc.quads != nullptr);
+    var = effective_variant(first, var, gp->sc.quads != nullptr);
     if (first) {
         if (bvh) launch_bounce_v<true, true>(var, grid, in, out, b);
         else launch_bounce_v<true, false>(var, grid, in, out, b);
@@ -1096,24 +1118,24 @@ template <int CITEMS>
 void launch_compact(PathBuf pi, PathBuf po, const int* n_in, int* n_out, int npaths) {
     constexpr int CTILE = BLOCK * CITEMS;
     const int ntiles = (npaths + CTILE - 1) / CTILE;
-    launch(5, k_compact_count<CITEMS>, dim3(ntiles), dim3(BLOCK), 0, (const int*)g.d_alive, n_in, g.d_tile_cnt);
-    launch(5, k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, (const int*)g.d_tile_cnt, n_in, g.d_tile_off, n_out,
+    launch(5, k_compact_count<CITEMS>, dim3(ntiles), dim3(BLOCK), 0, (const int*)gp->d_alive, n_in, gp->d_tile_cnt);
+    launch(5, k_compact_scan, dim3(1), dim3(SCAN_THREADS), 0, (const int*)gp->d_tile_cnt, n_in, gp->d_tile_off, n_out,
            CTILE);
     launch(3, k_compact_scatter<CITEMS>, dim3(ntiles), dim3(BLOCK), 0, (const float4*)pi.A, (const float4*)pi.B,
-           (const float4*)pi.C, po.A, po.B, po.C, (const int*)g.d_alive, n_in, (const int*)g.d_tile_off);
+           (const float4*)pi.C, po.A, po.B, po.C, (const int*)gp->d_alive, n_in, (const int*)gp->d_tile_off);
 }
 
-// Enqueue one pass's kernels (everything after k_frame_begin) on g.stream: `batch` frames
+// Enqueue one pass's kernels (everything after k_frame_begin) on gp->stream: `batch` frames
 // traced together as one wavefront of local_pixels x batch paths.
 // single-frame passes of primitive-only scenes run bounces tail_from() .. depth-1 as one k_tail
 // launch (PT_TAIL=0 turns it off for A/B); 0: no tail launch
 int tail_from(int batch) {
     static const bool off = getenv("PT_TAIL") && atoi(getenv("PT_TAIL")) == 0;
-    const int depth = g.sc.trace_depth;
-    const bool lds = g.sc.num_geoms <= LDS_GEOMS;
+    const int depth = gp->sc.trace_depth;
+    const bool lds = gp->sc.num_geoms <= LDS_GEOMS;
     static const bool any_batch = getenv("PT_TAIL_BATCH") && atoi(getenv("PT_TAIL_BATCH")) != 0;   // tools: A/B
-    if (off || (batch != 1 && !any_batch) || g.has_bvh || !lds || depth < 3 ||
-        (effective_variant(false, g.opts.variant, false) & ~VAR_NO_TEX) !=
+    if (off || (batch != 1 && !any_batch) || gp->has_bvh || !lds || depth < 3 ||
+        (effective_variant(false, gp->opts.variant, false) & ~VAR_NO_TEX) !=
             (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
         return 0;
     static const int from = getenv("PT_TAIL_FROM") ? atoi(getenv("PT_TAIL_FROM")) : 0;   // tools: A/B
@@ -1121,63 +1143,63 @@ int tail_from(int batch) {
 }
 
 int enqueue_pass_body(int batch) {
-    const int depth = g.sc.trace_depth;
-    const int npaths = g.local_pixels * batch;
+    const int depth = gp->sc.trace_depth;
+    const int npaths = gp->local_pixels * batch;
     const int nb = nblocks(npaths);
     const int nbounces = std::max(1, depth);
-    if (g.opts.pipeline == PT_PIPELINE_FUSED) {
+    if (gp->opts.pipeline == PT_PIPELINE_FUSED) {
         const int t = tail_from(batch);
         for (int b = 0; b < (t ? t : nbounces); ++b) {
             PathBuf in = pathbuf(b & 1), out = pathbuf((b + 1) & 1);
-            launch_bounce(b == 0, g.has_bvh, g.opts.variant & ~VAR_BVH_NODES, dim3(nb), in, out, b);
+            launch_bounce(b == 0, gp->has_bvh, gp->opts.variant & ~VAR_BVH_NODES, dim3(nb), in, out, b);
             HIPCHK(hipGetLastError());
         }
         if (t) {
             constexpr int V = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST;
-            const size_t lds = sizeof(DevGeomHot) * g.sc.num_geoms + sizeof(BlockLds);
-            if (g.no_tex)
-                launch(300 + t, k_tail<V | VAR_NO_TEX>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl,
-                       g.d_image, t, g.seg_stride, depth);
+            const size_t lds = sizeof(DevGeomHot) * gp->sc.num_geoms + sizeof(BlockLds);
+            if (gp->no_tex)
+                launch(300 + t, k_tail<V | VAR_NO_TEX>, dim3(nb), dim3(BLOCK), lds, gp->sc, pathbuf(t & 1), gp->d_ctl,
+                       gp->d_image, t, gp->seg_stride, depth);
             else
-                launch(300 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, g.sc, pathbuf(t & 1), g.d_ctl, g.d_image, t,
-                       g.seg_stride, depth);
+                launch(300 + t, k_tail<V>, dim3(nb), dim3(BLOCK), lds, gp->sc, pathbuf(t & 1), gp->d_ctl, gp->d_image, t,
+                       gp->seg_stride, depth);
             HIPCHK(hipGetLastError());
         }
         return PT_OK;
     }
     // STAGED (k_combine after the pass is enqueued by enqueue_pass)
     // STAGED
-    launch(0, k_camera, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(0), g.d_ctl);
+    launch(0, k_camera, dim3(nb), dim3(BLOCK), 0, gp->sc, pathbuf(0), gp->d_ctl);
     HIPCHK(hipGetLastError());
     const int stiles = (npaths + STILE - 1) / STILE;   // material-sort tiles
     int cur = 0;
     for (int b = 0; b < nbounces; ++b) {
         // compaction off: paths never move, every bounce sees all of them (pathtrace.cu:690)
-        const int* n_in = g.opts.stream_compaction ? staged_count(b) : staged_count(0);
-        HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
-        if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
-            launch(1, k_intersect<true, true>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
-        else if (g.has_bvh)
-            launch(1, k_intersect<true, false>, dim3(nb), dim3(BLOCK), g.bvh_lds, g.sc, pathbuf(cur), hits, n_in);
+        const int* n_in = gp->opts.stream_compaction ? staged_count(b) : staged_count(0);
+        HitBuf hits{gp->d_hit_nt, gp->d_hit_mat, gp->d_hit_uvd0, gp->d_hit_uvd1};
+        if (gp->has_bvh && (gp->opts.variant & VAR_BVH_FAST))
+            launch(1, k_intersect<true, true>, dim3(nb), dim3(BLOCK), gp->bvh_lds, gp->sc, pathbuf(cur), hits, n_in);
+        else if (gp->has_bvh)
+            launch(1, k_intersect<true, false>, dim3(nb), dim3(BLOCK), gp->bvh_lds, gp->sc, pathbuf(cur), hits, n_in);
         else
-            launch(1, k_intersect<false, false>, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, n_in);
+            launch(1, k_intersect<false, false>, dim3(nb), dim3(BLOCK), 0, gp->sc, pathbuf(cur), hits, n_in);
         HIPCHK(hipGetLastError());
         const int* perm = nullptr;
-        if (g.opts.material_sort) {
-            const int nk = std::max(1, g.sc.num_mats);
-            launch(4, k_sort_hist, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.d_tile_hist);
-            launch(4, k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, g.d_tile_hist, n_in, nk);
-            launch(4, k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, (const int*)g.d_hit_mat, n_in, nk, g.key_bits,
-                   (const int*)g.d_tile_hist, g.d_perm);
+        if (gp->opts.material_sort) {
+            const int nk = std::max(1, gp->sc.num_mats);
+            launch(4, k_sort_hist, dim3(stiles), dim3(BLOCK), 0, (const int*)gp->d_hit_mat, n_in, nk, gp->d_tile_hist);
+            launch(4, k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, gp->d_tile_hist, n_in, nk);
+            launch(4, k_sort_scatter, dim3(stiles), dim3(BLOCK), 0, (const int*)gp->d_hit_mat, n_in, nk, gp->key_bits,
+                   (const int*)gp->d_tile_hist, gp->d_perm);
             HIPCHK(hipGetLastError());
-            perm = g.d_perm;
+            perm = gp->d_perm;
         }
-        launch(2, k_shade, dim3(nb), dim3(BLOCK), 0, g.sc, pathbuf(cur), hits, perm, n_in, (const FrameCtl*)g.d_ctl,
-               0, g.d_image, g.opts.stream_compaction ? g.d_alive : (int*)nullptr);
+        launch(2, k_shade, dim3(nb), dim3(BLOCK), 0, gp->sc, pathbuf(cur), hits, perm, n_in, (const FrameCtl*)gp->d_ctl,
+               0, gp->d_image, gp->opts.stream_compaction ? gp->d_alive : (int*)nullptr);
         HIPCHK(hipGetLastError());
-        if (g.opts.stream_compaction) {
+        if (gp->opts.stream_compaction) {
             PathBuf pi = pathbuf(cur), po = pathbuf(cur ^ 1);
-            int* n_out = &g.d_ctl->cnt[b + 1][0][0];
+            int* n_out = &gp->d_ctl->cnt[b + 1][0][0];
             launch_compact<CITEMS>(pi, po, n_in, n_out, npaths);
             HIPCHK(hipGetLastError());
             cur ^= 1;
@@ -1187,42 +1209,42 @@ int enqueue_pass_body(int batch) {
 }
 
 int enqueue_pass(int set_iter, int batch) {
-    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, g.d_ctl, set_iter, g.local_pixels, batch);
+    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, gp->d_ctl, set_iter, gp->local_pixels, batch);
     HIPCHK(hipGetLastError());
     RC(enqueue_pass_body(batch));
     if (batch > 1) {
-        launch(6, k_combine, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.sc, (const FrameCtl*)g.d_ctl,
-               g.d_image);
+        launch(6, k_combine, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->sc, (const FrameCtl*)gp->d_ctl,
+               gp->d_image);
         HIPCHK(hipGetLastError());
     }
     return PT_OK;
 }
 
 int build_graph(int batch) {
-    HIPCHK(hipStreamBeginCapture(g.stream, hipStreamCaptureModeThreadLocal));
+    HIPCHK(hipStreamBeginCapture(gp->stream, hipStreamCaptureModeThreadLocal));
     int rc = enqueue_pass(0, batch);
     hipGraph_t gr = nullptr;
-    hipError_t e = hipStreamEndCapture(g.stream, &gr);
+    hipError_t e = hipStreamEndCapture(gp->stream, &gr);
     if (rc != PT_OK) return rc;
     HIPCHK(e);
-    g.graph[batch] = gr;
-    HIPCHK(hipGraphInstantiate(&g.graph_exec[batch], gr, nullptr, nullptr, 0));
+    gp->graph[batch] = gr;
+    HIPCHK(hipGraphInstantiate(&gp->graph_exec[batch], gr, nullptr, nullptr, 0));
     return PT_OK;
 }
 
 // one pass: frames iter .. iter + batch - 1
 int run_pass(int iter, int batch) {
     RC(ensure_frames(batch));
-    if (g.opts.use_graph) {
-        if (!g.graph_exec[batch]) RC(build_graph(batch));
+    if (gp->opts.use_graph) {
+        if (!gp->graph_exec[batch]) RC(build_graph(batch));
         // the graph's k_frame_begin increments: preset iter - 1 (stream-ordered)
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&g.d_ctl->iter, iter - 1, 1, g.stream));
-        HIPCHK(hipGraphLaunch(g.graph_exec[batch], g.stream));
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&gp->d_ctl->iter, iter - 1, 1, gp->stream));
+        HIPCHK(hipGraphLaunch(gp->graph_exec[batch], gp->stream));
     } else {
         RC(enqueue_pass(iter, batch));
     }
-    g.last_iter = iter + batch - 1;
-    g.frames_done += batch;
+    gp->last_iter = iter + batch - 1;
+    gp->frames_done += batch;
     return PT_OK;
 }
 int run_frame(int iter) { return run_pass(iter, 1); }
@@ -1231,7 +1253,7 @@ int run_frame(int iter) { return run_pass(iter, 1); }
 // (100 frames at F = 32 -> 4 x 25, not 32 + 32 + 32 + 4: a small last pass runs its launches
 // with a fraction of the paths in flight at nearly full per-launch cost)
 int pass_frames(int remaining) {
-    const int passes = (remaining + g.batch - 1) / g.batch;
+    const int passes = (remaining + gp->batch - 1) / gp->batch;
     return (remaining + passes - 1) / passes;
 }
 
@@ -1277,6 +1299,40 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
     return h;
 }
 
+// Every inner node's box contains both children's boxes and every leaf's box contains its
+// triangles' vertices, with ordered (non-NaN) bounds -- true of every tree scene.cpp:428-441
+// builds (each box is the min / max over its own triangles).  The reference then visits a leaf
+// iff the leaf's own box passes, which is what a different hierarchy above the
+// leaves and the certified t-culls need.  Called after the structural checks (children and
+// triIndices in range).
+bool bvh_boxes_nested(const pt_scene_view& s) {
+    auto inside = [](const pt_vec3& lo, const pt_vec3& hi, const pt_vec3& a, const pt_vec3& b) {
+        return lo.x <= a.x && lo.y <= a.y && lo.z <= a.z && b.x <= hi.x && b.y <= hi.y && b.z <= hi.z;
+    };
+    for (int i = 0; i < s.num_bvh_nodes; ++i) {
+        const pt_bvh_node& nd = s.bvh_nodes[i];
+        if (nd.triCount > 0 && nd.start >= 0) {
+            for (int k = 0; k < nd.triCount; ++k) {
+                const int64_t j = (int64_t)nd.start + k;
+                if (j >= s.num_tri_indices) return false;
+                const int ti = s.tri_indices[j];
+                if (ti < 0 || ti >= s.num_triangles) return false;
+                const pt_triangle& t = s.triangles[ti];
+                for (const pt_vertex* v : {&t.v1, &t.v2, &t.v3})
+                    if (!inside(nd.aabb.min, nd.aabb.max, v->position, v->position)) return false;
+            }
+            continue;
+        }
+        for (int c : {nd.left, nd.right}) {
+            if (c < 0) continue;
+            if (c >= s.num_bvh_nodes) return false;
+            const pt_bvh_node& ch = s.bvh_nodes[c];
+            if (!inside(nd.aabb.min, nd.aabb.max, ch.aabb.min, ch.aabb.max)) return false;
+        }
+    }
+    return true;
+}
+
 template <class T>
 void dfree(T*& p) {
     if (p) (void)hipFree((void*)p);
@@ -1286,50 +1342,50 @@ void dfree(T*& p) {
 // staged-pipeline buffers (hits, alive flags, permutation, tile counts): the staged pipeline and
 // the pt_test_* entry points use them; the fused pipeline never does
 void free_staged_buffers() {
-    dfree(g.d_hit_nt);
-    dfree(g.d_hit_mat);
-    dfree(g.d_hit_uvd0);
-    dfree(g.d_hit_uvd1);
-    dfree(g.d_alive);
-    dfree(g.d_perm);
-    dfree(g.d_tile_hist);
-    dfree(g.d_tile_cnt);
-    dfree(g.d_tile_off);
-    g.staged_alloc = false;
+    dfree(gp->d_hit_nt);
+    dfree(gp->d_hit_mat);
+    dfree(gp->d_hit_uvd0);
+    dfree(gp->d_hit_uvd1);
+    dfree(gp->d_alive);
+    dfree(gp->d_perm);
+    dfree(gp->d_tile_hist);
+    dfree(gp->d_tile_cnt);
+    dfree(gp->d_tile_off);
+    gp->staged_alloc = false;
 }
 void free_pass_buffers() {
     free_staged_buffers();
     for (int i = 0; i < 2; ++i)
-        for (int k = 0; k < 3; ++k) dfree(g.d_path[i][k]);
-    dfree(g.queue.A);
-    dfree(g.queue.B);
-    dfree(g.queue.C);
-    dfree(g.queue.D);
-    dfree(g.d_contrib);
-    g.sc.contrib = nullptr;
-    g.alloc_frames = 0;
-    g.seg_stride = 0;
-    g.capacity = 0;
+        for (int k = 0; k < 3; ++k) dfree(gp->d_path[i][k]);
+    dfree(gp->queue.A);
+    dfree(gp->queue.B);
+    dfree(gp->queue.C);
+    dfree(gp->queue.D);
+    dfree(gp->d_contrib);
+    gp->sc.contrib = nullptr;
+    gp->alloc_frames = 0;
+    gp->seg_stride = 0;
+    gp->capacity = 0;
 }
 
 // output segment s receives the survivors of the chunks c = s (mod NSEG): of k_bounce's, and in
 // split mode also of k_bvh_bounce's (its chunks of the queue) -- twice the room then
 int seg_stride_for(int frames) {
-    const int nb = nblocks(std::max(1, g.local_pixels * frames));
-    return ((nb + NSEG - 1) / NSEG) * BLOCK * (g.split ? 2 : 1);
+    const int nb = nblocks(std::max(1, gp->local_pixels * frames));
+    return ((nb + NSEG - 1) / NSEG) * BLOCK * (gp->split ? 2 : 1);
 }
 // paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
 int capacity_for(int frames) {
-    const int c = std::max(seg_stride_for(frames) * NSEG, g.local_pixels * frames);
+    const int c = std::max(seg_stride_for(frames) * NSEG, gp->local_pixels * frames);
     return ((c + STILE - 1) / STILE) * STILE;
 }
 // device bytes of the per-pass buffers for `frames` frames (auto F is capped by free memory)
 size_t pass_bytes(int frames, bool staged) {
     const size_t cap = (size_t)capacity_for(frames);
     size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
-    if (g.split) b += 4 * sizeof(float4) * (size_t)g.local_pixels * frames;       // traversal queue
-    if (frames > 1) b += 3 * sizeof(float) * (size_t)g.pixels_total * frames;      // contribution planes
-    if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (g.num_tex ? 2 * sizeof(float4) : 0));
+    if (gp->split) b += 4 * sizeof(float4) * (size_t)gp->local_pixels * frames;       // traversal queue
+    if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
+    if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
     return b;
 }
 
@@ -1337,72 +1393,74 @@ size_t pass_bytes(int frames, bool staged) {
 // Grows only; captured pass graphs hold the old pointers, so they are released on growth.
 int ensure_frames(int frames) {
     frames = std::max(1, frames);
-    if (frames <= g.alloc_frames) return PT_OK;
-    const bool staged = g.staged_alloc || g.opts.pipeline == PT_PIPELINE_STAGED;
+    if (frames <= gp->alloc_frames) return PT_OK;
+    const bool staged = gp->staged_alloc || gp->opts.pipeline == PT_PIPELINE_STAGED;
+    // a captured pass may still be running (pt_trace_frames does not wait): drain the stream
+    // before its graph and the buffers it reads go away
+    HIPCHK(hipStreamSynchronize(gp->stream));
     release_graph();
-    HIPCHK(hipStreamSynchronize(g.stream));
     free_pass_buffers();
-    g.seg_stride = seg_stride_for(frames);
-    g.capacity = capacity_for(frames);
+    gp->seg_stride = seg_stride_for(frames);
+    gp->capacity = capacity_for(frames);
     for (int i = 0; i < 2; ++i)
-        for (int k = 0; k < 3; ++k) RC(dalloc(&g.d_path[i][k], (size_t)g.capacity));
-    if (g.split) {
-        const size_t qn = (size_t)g.local_pixels * frames;
-        RC(dalloc(&g.queue.A, qn));
-        RC(dalloc(&g.queue.B, qn));
-        RC(dalloc(&g.queue.C, qn));
-        RC(dalloc(&g.queue.D, qn));
+        for (int k = 0; k < 3; ++k) RC(dalloc(&gp->d_path[i][k], (size_t)gp->capacity));
+    if (gp->split) {
+        const size_t qn = (size_t)gp->local_pixels * frames;
+        RC(dalloc(&gp->queue.A, qn));
+        RC(dalloc(&gp->queue.B, qn));
+        RC(dalloc(&gp->queue.C, qn));
+        RC(dalloc(&gp->queue.D, qn));
     }
-    if (frames > 1) RC(dalloc(&g.d_contrib, (size_t)g.pixels_total * 3 * frames));
-    g.sc.contrib = g.d_contrib;
-    g.alloc_frames = frames;
+    if (frames > 1) RC(dalloc(&gp->d_contrib, (size_t)gp->pixels_total * 3 * frames));
+    gp->sc.contrib = gp->d_contrib;
+    gp->alloc_frames = frames;
     if (staged) {
-        RC(dalloc(&g.d_hit_nt, (size_t)g.capacity));
-        RC(dalloc(&g.d_hit_mat, (size_t)g.capacity));
-        if (g.num_tex) {
-            RC(dalloc(&g.d_hit_uvd0, (size_t)g.capacity));
-            RC(dalloc(&g.d_hit_uvd1, (size_t)g.capacity));
+        RC(dalloc(&gp->d_hit_nt, (size_t)gp->capacity));
+        RC(dalloc(&gp->d_hit_mat, (size_t)gp->capacity));
+        if (gp->num_tex) {
+            RC(dalloc(&gp->d_hit_uvd0, (size_t)gp->capacity));
+            RC(dalloc(&gp->d_hit_uvd1, (size_t)gp->capacity));
         }
-        RC(dalloc(&g.d_alive, (size_t)g.capacity));
-        RC(dalloc(&g.d_perm, (size_t)g.capacity));
-        const int ntiles = (g.capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
-        RC(dalloc(&g.d_tile_hist, (size_t)ntiles * std::max(1, g.sc.num_mats)));
-        RC(dalloc(&g.d_tile_cnt, (size_t)ntiles));
-        RC(dalloc(&g.d_tile_off, (size_t)ntiles));
-        g.staged_alloc = true;
+        RC(dalloc(&gp->d_alive, (size_t)gp->capacity));
+        RC(dalloc(&gp->d_perm, (size_t)gp->capacity));
+        const int ntiles = (gp->capacity + CTILE_MIN - 1) / CTILE_MIN + 1;
+        RC(dalloc(&gp->d_tile_hist, (size_t)ntiles * std::max(1, gp->sc.num_mats)));
+        RC(dalloc(&gp->d_tile_cnt, (size_t)ntiles));
+        RC(dalloc(&gp->d_tile_off, (size_t)ntiles));
+        gp->staged_alloc = true;
     }
     return PT_OK;
 }
 // the staged buffers at the current capacity (the pt_test_* entry points under the fused pipeline)
 int ensure_staged() {
-    if (g.staged_alloc) return PT_OK;
-    const int f = std::max(1, g.alloc_frames);
-    g.alloc_frames = 0;              // re-size everything with the staged buffers included
-    g.staged_alloc = true;
+    if (gp->staged_alloc) return PT_OK;
+    const int f = std::max(1, gp->alloc_frames);
+    gp->alloc_frames = 0;              // re-size everything with the staged buffers included
+    gp->staged_alloc = true;
     return ensure_frames(f);
 }
-// a pt_test_* call on n paths: room for n (up to what a pass of g.batch frames holds) + staged buffers
+// a pt_test_* call on n paths: room for n (up to what a pass of gp->batch frames holds) + staged buffers
 int ensure_test_paths(int64_t n) {
-    const int64_t most = capacity_for(g.batch);
+    const int64_t most = capacity_for(gp->batch);
     if (n < 0 || n > most) return fail(PT_E_INVALID, "n out of range (capacity %lld)", (long long)most);
     RC(ensure_staged());
-    const int frames = (int)std::min<int64_t>(g.batch, std::max<int64_t>(1, (n + g.local_pixels - 1) / g.local_pixels));
+    const int frames = (int)std::min<int64_t>(gp->batch, std::max<int64_t>(1, (n + gp->local_pixels - 1) / gp->local_pixels));
     RC(ensure_frames(frames));
-    if (n > g.capacity) return fail(PT_E_INVALID, "n out of range (capacity %d)", g.capacity);
+    if (n > gp->capacity) return fail(PT_E_INVALID, "n out of range (capacity %d)", gp->capacity);
     return PT_OK;
 }
 
 void free_all() {
     release_graph();
     free_pass_buffers();
-    void* ptrs[] = {g.d_geoms, g.d_cull, g.d_mats, g.d_nodes, g.d_node_aux, g.d_hot, g.d_pairs, g.d_quads, g.d_hot4,
-                    g.d_leaf9, g.d_cold, g.d_texels, g.d_texinfo, g.d_image, g.d_ctl};
+    void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_quads, gp->d_hot4,
+                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    if (g.stream) (void)hipStreamDestroy(g.stream);
-    int32_t* td = g.traced_depth;
-    g = State();
-    g.traced_depth = td;
+    if (gp->stream) (void)hipStreamDestroy(gp->stream);
+    int32_t* td = gp->traced_depth;
+    *gp = State();
+    gp->traced_depth = td;
 }
 
 template <class T>
@@ -1456,25 +1514,290 @@ void soa_to_paths(const std::vector<float4>& A, const std::vector<float4>& B, co
 int upload_paths(int buf, const pt_path_segment* paths, int64_t n) {
     std::vector<float4> A, B, C;
     paths_to_soa(paths, n, A, B, C);
-    HIPCHK(smemcpy(g.d_path[buf][0], A.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(smemcpy(g.d_path[buf][1], B.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(smemcpy(g.d_path[buf][2], C.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(gp->d_path[buf][0], A.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(gp->d_path[buf][1], B.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(gp->d_path[buf][2], C.data(), n * sizeof(float4), hipMemcpyHostToDevice));
     return PT_OK;
 }
 int download_paths(int buf, int64_t n, pt_path_segment* out) {
     std::vector<float4> A(n), B(n), C(n);
-    HIPCHK(smemcpy(A.data(), g.d_path[buf][0], n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(smemcpy(B.data(), g.d_path[buf][1], n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(smemcpy(C.data(), g.d_path[buf][2], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(A.data(), gp->d_path[buf][0], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(B.data(), gp->d_path[buf][1], n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(C.data(), gp->d_path[buf][2], n * sizeof(float4), hipMemcpyDeviceToHost));
     soa_to_paths(A, B, C, n, out);
     return PT_OK;
 }
 int set_count(int slot, int value) {
-    HIPCHK(smemcpy(&g.d_ctl->cnt[slot][0][0], &value, sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(&gp->d_ctl->cnt[slot][0][0], &value, sizeof(int), hipMemcpyHostToDevice));
     return PT_OK;
 }
 
-int need_init() { return g.inited ? PT_OK : fail(PT_E_STATE, "pt_init has not been called"); }
+int need_init() { return gp->inited ? PT_OK : fail(PT_E_STATE, "pt_init has not been called"); }
+
+// ---------------------------------------------------------------------------------------------
+// Several GPUs behind one pathtrace() (pt_options.num_devices > 1; SURVEY §8b: the split is
+// internal to the boundary).  Shard k is a whole context of its own (State: device, stream,
+// scene copy, pass buffers, full-size image of which it writes only its pixels) tracing the
+// interleaved row bands (y / rows) % N == k; pixels are independent (the RNG is keyed by pixel,
+// iteration and depth), so the shards need no exchange while tracing.  After every call the
+// first device's image receives every shard's pixels: a pull kernel over xGMI peer access (or a
+// packed tile + hipMemcpyPeerAsync without it), or one RCCL group of send / recv.
+// ---------------------------------------------------------------------------------------------
+struct Rccl {   // librccl.so, opened at the first pt_init that asks for it (the library is ~570 MB)
+    void* h = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+Rccl g_rccl;
+
+int rccl_open() {
+    if (g_rccl.h) return PT_OK;
+    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return fail(PT_E_UNSUPPORTED, "PT_COMBINE_RCCL: cannot load librccl.so: %s", dlerror());
+    Rccl r;
+    r.h = h;
+#define PT_RCCL_SYM(f)                                                             \
+    r.f = reinterpret_cast<decltype(r.f)>(dlsym(h, "nccl" #f));                    \
+    if (!r.f) {                                                                    \
+        dlclose(h);                                                                \
+        return fail(PT_E_UNSUPPORTED, "PT_COMBINE_RCCL: librccl.so lacks nccl" #f); \
+    }
+    PT_RCCL_SYM(CommInitAll)
+    PT_RCCL_SYM(CommDestroy)
+    PT_RCCL_SYM(GroupStart)
+    PT_RCCL_SYM(GroupEnd)
+    PT_RCCL_SYM(Send)
+    PT_RCCL_SYM(Recv)
+    PT_RCCL_SYM(GetErrorString)
+#undef PT_RCCL_SYM
+    g_rccl = r;
+    return PT_OK;
+}
+#define NCCLCHK(expr)                                                                                   \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess)                                                                          \
+            return fail(PT_E_HIP, "%s:%d: %s: %s", __FILE__, __LINE__, #expr, g_rccl.GetErrorString(r_)); \
+    } while (0)
+
+struct Multi {
+    int n = 0;                                     // shard contexts (0: single-context mode)
+    State* shard[PT_MAX_DEVICES] = {};             // shard[0] == &g_primary
+    int combine = PT_COMBINE_PEER;
+    hipEvent_t done[PT_MAX_DEVICES] = {};          // shard k's queued work (its stream, its device)
+    hipEvent_t pulled = nullptr;                   // the first device finished reading the shards
+    bool direct[PT_MAX_DEVICES] = {};              // PEER: the first device reads shard k's image itself
+    float* tile[PT_MAX_DEVICES] = {};              // shard k's packed pixels on its device (RCCL, staged peer)
+    float* recv[PT_MAX_DEVICES] = {};              // the same on the first device
+    // RCCL: one communicator rank per distinct device, each with its own stream
+    int ndist = 0;
+    int dist_dev[PT_MAX_DEVICES] = {};
+    int dist_of[PT_MAX_DEVICES] = {};              // shard k -> index of its device in dist_dev
+    ncclComm_t comm[PT_MAX_DEVICES] = {};
+    hipStream_t cstream[PT_MAX_DEVICES] = {};
+    hipEvent_t cdone[PT_MAX_DEVICES] = {};
+};
+Multi M;
+
+int nshards() { return M.n > 1 ? M.n : 1; }
+State* shard_ctx(int k) { return M.n > 1 ? M.shard[k] : &g_primary; }
+
+// the host runtime works on one shard (its context and its device) until the scope ends
+struct ShardScope {
+    State* prev;
+    int prev_dev = 0;
+    explicit ShardScope(State* s) : prev(gp) {
+        (void)hipGetDevice(&prev_dev);
+        gp = s;
+        (void)hipSetDevice(s->device);
+    }
+    ~ShardScope() {
+        gp = prev;
+        (void)hipSetDevice(prev_dev);
+    }
+};
+
+int need_single(const char* what) {
+    return M.n > 1 ? fail(PT_E_UNSUPPORTED, "%s: one device context only (pt_options.num_devices > 1)", what) : PT_OK;
+}
+
+void multi_release() {
+    if (M.n <= 1) return;
+    int entry_dev = 0;
+    (void)hipGetDevice(&entry_dev);
+    for (int i = 0; i < M.ndist; ++i) {
+        (void)hipSetDevice(M.dist_dev[i]);
+        if (M.comm[i] && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(M.comm[i]);
+        if (M.cdone[i]) (void)hipEventDestroy(M.cdone[i]);
+        if (M.cstream[i]) (void)hipStreamDestroy(M.cstream[i]);
+    }
+    for (int k = 0; k < M.n; ++k) {
+        State* s = M.shard[k];
+        if (!s) continue;
+        (void)hipSetDevice(s->device);
+        if (M.done[k]) (void)hipEventDestroy(M.done[k]);
+        if (M.tile[k]) (void)hipFree(M.tile[k]);
+    }
+    (void)hipSetDevice(M.shard[0] ? M.shard[0]->device : 0);
+    for (int k = 0; k < M.n; ++k)
+        if (M.recv[k]) (void)hipFree(M.recv[k]);
+    if (M.pulled) (void)hipEventDestroy(M.pulled);
+    (void)hipSetDevice(entry_dev);
+}
+
+// events, peer access, tiles and (RCCL) communicators once every shard is initialised
+int multi_setup() {
+    State* p = M.shard[0];
+    ShardScope entry(p);   // restores the caller's device and context last
+    for (int k = 0; k < M.n; ++k) {
+        ShardScope sc(M.shard[k]);
+        HIPCHK(hipEventCreateWithFlags(&M.done[k], hipEventDisableTiming));
+    }
+    {
+        ShardScope sc(p);
+        HIPCHK(hipEventCreateWithFlags(&M.pulled, hipEventDisableTiming));
+    }
+    const size_t W = (size_t)p->width;
+    for (int k = 1; k < M.n; ++k) {
+        State* s = M.shard[k];
+        const size_t bytes = 3 * sizeof(float) * (size_t)std::max(1, s->local_pixels);
+        bool direct = M.combine == PT_COMBINE_PEER && s->device == p->device;
+        if (M.combine == PT_COMBINE_PEER && !direct) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, p->device, s->device) == hipSuccess && can) {
+                ShardScope sc(p);
+                const hipError_t e = hipDeviceEnablePeerAccess(s->device, 0);
+                if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) direct = true;
+                (void)hipGetLastError();
+            }
+        }
+        M.direct[k] = direct;
+        if (!direct) {   // packed tiles: RCCL, or peer copies without peer access
+            {
+                ShardScope sc(s);
+                RC(dalloc(&M.tile[k], bytes / sizeof(float)));
+            }
+            ShardScope sc(p);
+            RC(dalloc(&M.recv[k], bytes / sizeof(float)));
+        }
+    }
+    (void)W;
+    if (M.combine != PT_COMBINE_RCCL) return PT_OK;
+    RC(rccl_open());
+    for (int k = 0; k < M.n; ++k) {
+        int i = 0;
+        while (i < M.ndist && M.dist_dev[i] != M.shard[k]->device) ++i;
+        if (i == M.ndist) M.dist_dev[M.ndist++] = M.shard[k]->device;
+        M.dist_of[k] = i;
+    }
+    NCCLCHK(g_rccl.CommInitAll(M.comm, M.ndist, M.dist_dev));
+    for (int i = 0; i < M.ndist; ++i) {
+        HIPCHK(hipSetDevice(M.dist_dev[i]));
+        HIPCHK(hipStreamCreateWithFlags(&M.cstream[i], hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&M.cdone[i], hipEventDisableTiming));
+    }
+    HIPCHK(hipSetDevice(p->device));
+    return PT_OK;
+}
+
+// every shard's pixels into the first device's image, ordered after the work queued so far on
+// every shard's stream; the shards' next work waits until the first device has read them
+int multi_combine() {
+    if (M.n <= 1) return PT_OK;
+    State* p = M.shard[0];
+    ShardScope entry(p);   // restores the caller's device and context last
+    const int W = p->width;
+    for (int k = 1; k < M.n; ++k) {
+        State* s = M.shard[k];
+        ShardScope sc(s);
+        if (!M.direct[k]) {
+            hipLaunchKernelGGL(k_pack_tile, dim3(nblocks(s->local_pixels)), dim3(BLOCK), 0, s->stream, s->d_image,
+                               s->sc.shard, W, M.tile[k]);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipEventRecord(M.done[k], s->stream));
+    }
+    if (M.combine == PT_COMBINE_RCCL) {
+        const int d0 = M.dist_of[0];
+        {   // the first device's receive buffers are free once its earlier unpacks ran
+            ShardScope sc(p);
+            HIPCHK(hipEventRecord(M.done[0], p->stream));
+        }
+        for (int k = 0; k < M.n; ++k) {
+            HIPCHK(hipSetDevice(M.dist_dev[M.dist_of[k]]));
+            HIPCHK(hipStreamWaitEvent(M.cstream[M.dist_of[k]], M.done[k], 0));
+        }
+        NCCLCHK(g_rccl.GroupStart());
+        for (int k = 1; k < M.n; ++k) {
+            const size_t cnt = 3 * (size_t)M.shard[k]->local_pixels;
+            const int dk = M.dist_of[k];
+            NCCLCHK(g_rccl.Send(M.tile[k], cnt, ncclFloat32, d0, M.comm[dk], M.cstream[dk]));
+            NCCLCHK(g_rccl.Recv(M.recv[k], cnt, ncclFloat32, dk, M.comm[d0], M.cstream[d0]));
+        }
+        NCCLCHK(g_rccl.GroupEnd());
+        for (int i = 0; i < M.ndist; ++i) {
+            HIPCHK(hipSetDevice(M.dist_dev[i]));
+            HIPCHK(hipEventRecord(M.cdone[i], M.cstream[i]));
+        }
+        for (int k = 1; k < M.n; ++k) {   // a tile is rewritten only after its send completed
+            ShardScope sc(M.shard[k]);
+            HIPCHK(hipStreamWaitEvent(M.shard[k]->stream, M.cdone[M.dist_of[k]], 0));
+        }
+        ShardScope sc(p);
+        HIPCHK(hipStreamWaitEvent(p->stream, M.cdone[d0], 0));
+        for (int k = 1; k < M.n; ++k) {
+            hipLaunchKernelGGL(k_unpack_tile, dim3(nblocks(M.shard[k]->local_pixels)), dim3(BLOCK), 0, p->stream,
+                               p->d_image, M.shard[k]->sc.shard, W, (const float*)M.recv[k]);
+            HIPCHK(hipGetLastError());
+        }
+        return PT_OK;
+    }
+    ShardScope sc(p);
+    for (int k = 1; k < M.n; ++k) {
+        State* s = M.shard[k];
+        HIPCHK(hipStreamWaitEvent(p->stream, M.done[k], 0));
+        if (M.direct[k]) {
+            hipLaunchKernelGGL(k_pull_shard, dim3(nblocks(s->local_pixels)), dim3(BLOCK), 0, p->stream, p->d_image,
+                               s->sc.shard, W, (const float*)s->d_image);
+        } else {
+            HIPCHK(hipMemcpyPeerAsync(M.recv[k], p->device, M.tile[k], s->device,
+                                      3 * sizeof(float) * (size_t)s->local_pixels, p->stream));
+            hipLaunchKernelGGL(k_unpack_tile, dim3(nblocks(s->local_pixels)), dim3(BLOCK), 0, p->stream, p->d_image,
+                               s->sc.shard, W, (const float*)M.recv[k]);
+        }
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(M.pulled, p->stream));
+    for (int k = 1; k < M.n; ++k) {   // a shard's image changes again only after it was read
+        ShardScope s2(M.shard[k]);
+        HIPCHK(hipStreamWaitEvent(M.shard[k]->stream, M.pulled, 0));
+    }
+    return PT_OK;
+}
+
+// GuiDataContainer::TracedDepth of the last single-frame pass of the current context: the loop
+// stops after bounce k when no path is left alive, or at traceDepth (pathtrace.cu:759-770)
+int frame_depth(int& depth) {
+    depth = std::max(1, gp->sc.trace_depth);
+    if (!gp->opts.stream_compaction) return PT_OK;
+    std::vector<int> cnt((size_t)depth * NSEG * CNT_PAD);
+    HIPCHK(smemcpy(cnt.data(), &gp->d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int k = 1; k < depth; ++k) {
+        int64_t live = 0;
+        for (int q = 0; q < NSEG; ++q) live += cnt[((size_t)k * NSEG + q) * CNT_PAD];
+        if (live == 0) {
+            depth = k;
+            break;
+        }
+    }
+    return PT_OK;
+}
 
 }  // namespace
 
@@ -1503,16 +1826,50 @@ void pt_default_options(pt_options* o) {
     // fastest in the in-process A/B (tools/ab_variants.py); every variant is bit-identical
     o->variant = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BVH_SPLIT | VAR_BLOCK_REDIST;
     o->frames_per_pass = 0;        // auto
+    // several GPUs behind one pathtrace(): the drop-in and pt_render reach it through the environment
+    o->num_devices = 0;
+    for (int k = 0; k < PT_MAX_DEVICES; ++k) o->device_ids[k] = k;
+    if (const char* e = getenv("PT_DEVICES")) {
+        if (strchr(e, ',')) {
+            int n = 0;
+            for (const char* c = e; *c && n < PT_MAX_DEVICES;) {
+                char* end = nullptr;
+                const long v = strtol(c, &end, 10);
+                if (end == c) break;
+                o->device_ids[n++] = (int32_t)v;
+                c = *end == ',' ? end + 1 : end;
+                if (*end != ',') break;
+            }
+            o->num_devices = n;
+        } else {
+            o->num_devices = (int32_t)std::min<long>(PT_MAX_DEVICES, std::max<long>(0, strtol(e, nullptr, 10)));
+        }
+    }
+    o->combine = PT_COMBINE_PEER;
+    if (const char* e = getenv("PT_COMBINE")) o->combine = strcmp(e, "rccl") == 0 ? PT_COMBINE_RCCL : PT_COMBINE_PEER;
 }
 
 int32_t pt_init_data_container(int32_t* traced_depth) {
-    g.traced_depth = traced_depth;
+    gp->traced_depth = traced_depth;
     return PT_OK;
 }
 
 int32_t pt_free(void) {
-    if (g.inited) free_all();
-    g.inited = false;
+    gp = &g_primary;
+    if (M.n > 1) {
+        multi_release();
+        for (int k = M.n - 1; k >= 1; --k) {
+            if (!M.shard[k]) continue;
+            {
+                ShardScope sc(M.shard[k]);
+                if (gp->inited) free_all();
+            }
+            delete M.shard[k];
+        }
+    }
+    M = Multi();
+    if (gp->inited) free_all();
+    gp->inited = false;
     return PT_OK;
 }
 
@@ -1525,12 +1882,9 @@ int auto_batch(int local_pixels) {
     return f;
 }
 
-int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
-    if (!s) return fail(PT_E_INVALID, "scene is NULL");
-    pt_free();
-    pt_options o;
-    if (opts_in) o = *opts_in;
-    else pt_default_options(&o);
+// one context (gp): the whole pathtraceInit for one device, or for shard k of a multi-device
+// context; `share` contexts live on this device (auto F divides its free memory among them)
+static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     if (o.block_size != BLOCK) return fail(PT_E_UNSUPPORTED, "block_size must be %d", BLOCK);
     const int W = s->camera.resolution.x, H = s->camera.resolution.y;
     if (W <= 0 || H <= 0) return fail(PT_E_INVALID, "bad resolution %dx%d", W, H);
@@ -1542,12 +1896,12 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
     if (o.device < 0 || o.device >= ndev) return fail(PT_E_INVALID, "device %d out of range", o.device);
     HIPCHK(hipSetDevice(o.device));
-    g.opts = o;
-    g.device = o.device;
-    HIPCHK(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-    g.width = W;
-    g.height = H;
-    g.pixels_total = W * H;
+    gp->opts = o;
+    gp->device = o.device;
+    HIPCHK(hipStreamCreateWithFlags(&gp->stream, hipStreamNonBlocking));
+    gp->width = W;
+    gp->height = H;
+    gp->pixels_total = W * H;
     // shard
     ShardDev sh{};
     sh.mode = o.shard_mode == PT_SHARD_PIXELS && o.shard_count > 1 ? 1 : 0;
@@ -1560,9 +1914,9 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         for (int y = 0; y < H; ++y) rows += ((y / sh.rows) % sh.count) == sh.rank;
         sh.local_pixels = rows * W;
     } else {
-        sh.local_pixels = g.pixels_total;
+        sh.local_pixels = gp->pixels_total;
     }
-    g.local_pixels = sh.local_pixels;
+    gp->local_pixels = sh.local_pixels;
     if (o.frames_per_pass < 0 || o.frames_per_pass > MAXF)
         return fail(PT_E_INVALID, "frames_per_pass must be 0 (auto) .. %d", MAXF);
 
@@ -1689,11 +2043,11 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         d.bumpScale = m.bumpScale;
     }
     // no material samples a texture or bump map: the fused kernels' texture-free build (VAR_NO_TEX)
-    g.no_tex = true;
+    gp->no_tex = true;
     for (int i = 0; i < s->num_materials; ++i)
-        if (s->materials[i].hasTexture || s->materials[i].hasBumpMap) g.no_tex = false;
+        if (s->materials[i].hasTexture || s->materials[i].hasBumpMap) gp->no_tex = false;
     // BVH: only when the reference would traverse it (BVH_ACCELERATION and a non-empty tree)
-    g.has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
+    gp->has_bvh = o.bvh && s->num_bvh_nodes > 0 && s->num_triangles > 0;
     std::vector<DevNode> nodes;
     std::vector<float4> node_aux;
     std::vector<DevTriHot> hot;
@@ -1706,7 +2060,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     int quad_root_ref = 0, quad_count = 0;
     float4 pair_root_lo{}, pair_root_hi{};
     double cull_extent = 1.0;
-    if (g.has_bvh) {
+    if (gp->has_bvh) {
         nodes.resize(s->num_bvh_nodes);
         for (int i = 0; i < s->num_bvh_nodes; ++i) {
             const pt_bvh_node& nd = s->bvh_nodes[i];
@@ -1845,12 +2199,15 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             return fail(PT_E_UNSUPPORTED, "BVH needs a %d-entry traversal stack; the reference's holds %d "
                         "(intersections.cu:167)", ref_stack, MAXSTACK);
         const int tree_height = bvh_height(s->bvh_nodes, s->num_bvh_nodes);
-        if (tree_height < 0 || tree_height + 1 > MAXSTACK) {
+        // the near-first traversals (pair layout, SAH hierarchy, certified t-culls) rely on the
+        // boxes being nested as scene.cpp:428-441 builds them; a caller-supplied tree that is not
+        // keeps the reference-order traversal, which assumes nothing
+        if (tree_height < 0 || tree_height + 1 > MAXSTACK || !bvh_boxes_nested(*s)) {
             o.variant &= ~(VAR_BVH_FAST | VAR_BVH_SPLIT);
-            g.opts.variant = o.variant;
+            gp->opts.variant = o.variant;
         }
-        g.stack_depth = std::max(2, ref_stack);
-        if (o.variant & VAR_BVH_FAST) g.stack_depth = std::max(g.stack_depth, tree_height + 1);
+        gp->stack_depth = std::max(2, ref_stack);
+        if (o.variant & VAR_BVH_FAST) gp->stack_depth = std::max(gp->stack_depth, tree_height + 1);
         // VAR_BVH_FAST pair layout (DevPair): walk the tree in the reference's visit order
         // (push left, push right, pop -> right subtree first), numbering internal nodes (pairs)
         // and leaves (4-slot triangle groups).  Any tree this layout cannot hold exactly -- a
@@ -1962,8 +2319,8 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                             *hi[k] = make_float4(c.hi[0], c.hi[1], c.hi[2], pack_cull(c.s));
                         }
                     }
-                    g.stack_depth = std::max(g.stack_depth, th + 1);
-                    g.pair_depth = th + 1;
+                    gp->stack_depth = std::max(gp->stack_depth, th + 1);
+                    gp->pair_depth = th + 1;
                     if (getenv("PT_BVH_TREE_INFO"))
                         fprintf(stderr, "pt_init: SAH traversal tree over %d reference leaves, height %d (reference %d)\n", L,
                                 th, height);
@@ -2064,23 +2421,23 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                         }
                         quad_count = Q;
                         quad_root_ref = is_leaf[0] ? id[0] : 0;
-                        g.stack_depth = std::max(g.stack_depth, 3 * qh + 1);
+                        gp->stack_depth = std::max(gp->stack_depth, 3 * qh + 1);
                     }
                 }
-                if (!sah) g.pair_depth = height + 1;
+                if (!sah) gp->pair_depth = height + 1;
                 pair_root_ref = sah ? 0 : ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;
             }
         }
-        g.bvh_lds = (size_t)g.stack_depth * BLOCK * sizeof(int);
+        gp->bvh_lds = (size_t)gp->stack_depth * BLOCK * sizeof(int);
     }
     for (int i = 0; i < s->num_geoms; ++i)
-        if (s->geoms[i].materialid >= std::max(1, s->num_materials))
+        if (s->geoms[i].materialid < 0 || s->geoms[i].materialid >= std::max(1, s->num_materials))
             return fail(PT_E_INVALID, "geom %d material %d out of range", i, s->geoms[i].materialid);
     // VAR_BVH_SPLIT needs the pair layout, the fast traversal and an LDS geom table
-    g.split = g.has_bvh && !pairs.empty() && o.pipeline == PT_PIPELINE_FUSED && (o.variant & VAR_BVH_SPLIT) &&
+    gp->split = gp->has_bvh && !pairs.empty() && o.pipeline == PT_PIPELINE_FUSED && (o.variant & VAR_BVH_SPLIT) &&
               (o.variant & VAR_BVH_FAST) && (o.variant & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) &&
               s->num_geoms <= LDS_GEOMS;
     // MATERIAL_SORTING on the fused pipeline: the block-local regrouping by material (VAR_MAT_GROUP;
@@ -2089,7 +2446,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         variant_compiled(effective_variant(true, o.variant | VAR_MAT_GROUP, !quads.empty())) &&
         variant_compiled(effective_variant(false, o.variant | VAR_MAT_GROUP, !quads.empty()))) {
         o.variant |= VAR_MAT_GROUP;
-        g.opts.variant = o.variant;
+        gp->opts.variant = o.variant;
     }
     if (o.pipeline == PT_PIPELINE_FUSED) {
         for (int first = 0; first < 2; ++first) {
@@ -2099,47 +2456,48 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
                             v, first ? "camera" : "later");
         }
     }
-    g.num_tex = (s->num_textures > 0 && s->textures) ? s->num_textures : 0;
-    g.sc.num_mats = s->num_materials;
+    gp->num_tex = (s->num_textures > 0 && s->textures) ? s->num_textures : 0;
+    gp->sc.num_mats = s->num_materials;
     // frames per pass: as asked, or auto (~84M paths), halved while the per-pass buffers would
     // take more than half of the device memory free now.  Buffers are allocated when a pass of
     // that size is first traced or prepared (ensure_frames), not here.
     if (o.frames_per_pass > 0) {
-        g.batch = o.frames_per_pass;
+        gp->batch = o.frames_per_pass;
     } else {
-        g.batch = auto_batch(g.local_pixels);
+        gp->batch = auto_batch(gp->local_pixels);
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-            while (g.batch > 1 && pass_bytes(g.batch, o.pipeline == PT_PIPELINE_STAGED) > free_b / 2) g.batch /= 2;
+            while (gp->batch > 1 && pass_bytes(gp->batch, o.pipeline == PT_PIPELINE_STAGED) > free_b / (2 * (size_t)share))
+                gp->batch /= 2;
     }
-    if ((int64_t)g.local_pixels * g.batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
+    if ((int64_t)gp->local_pixels * gp->batch > (1 << 28)) return fail(PT_E_UNSUPPORTED, "wavefront too large");
 
-    RC(dalloc(&g.d_geoms, geoms.size()));
-    RC(dalloc(&g.d_mats, mats.size()));
-    RC(upload(g.d_geoms, geoms.data(), geoms.size()));
-    RC(dalloc(&g.d_cull, culls.size()));
-    RC(upload(g.d_cull, culls.data(), culls.size()));
-    RC(upload(g.d_mats, mats.data(), mats.size()));
-    if (g.has_bvh) {
-        RC(dalloc(&g.d_nodes, nodes.size()));
-        RC(dalloc(&g.d_node_aux, node_aux.size()));
-        RC(upload(g.d_node_aux, node_aux.data(), node_aux.size()));
-        RC(dalloc(&g.d_hot, hot.size()));
-        RC(dalloc(&g.d_cold, cold.size()));
-        RC(upload(g.d_nodes, nodes.data(), nodes.size()));
-        RC(upload(g.d_hot, hot.data(), hot.size()));
-        RC(upload(g.d_cold, cold.data(), cold.size()));
+    RC(dalloc(&gp->d_geoms, geoms.size()));
+    RC(dalloc(&gp->d_mats, mats.size()));
+    RC(upload(gp->d_geoms, geoms.data(), geoms.size()));
+    RC(dalloc(&gp->d_cull, culls.size()));
+    RC(upload(gp->d_cull, culls.data(), culls.size()));
+    RC(upload(gp->d_mats, mats.data(), mats.size()));
+    if (gp->has_bvh) {
+        RC(dalloc(&gp->d_nodes, nodes.size()));
+        RC(dalloc(&gp->d_node_aux, node_aux.size()));
+        RC(upload(gp->d_node_aux, node_aux.data(), node_aux.size()));
+        RC(dalloc(&gp->d_hot, hot.size()));
+        RC(dalloc(&gp->d_cold, cold.size()));
+        RC(upload(gp->d_nodes, nodes.data(), nodes.size()));
+        RC(upload(gp->d_hot, hot.data(), hot.size()));
+        RC(upload(gp->d_cold, cold.data(), cold.size()));
         if (!quads.empty()) {
-            RC(dalloc(&g.d_quads, quads.size()));
-            RC(upload(g.d_quads, quads.data(), quads.size()));
+            RC(dalloc(&gp->d_quads, quads.size()));
+            RC(upload(gp->d_quads, quads.data(), quads.size()));
         }
         if (!pairs.empty()) {
-            RC(dalloc(&g.d_pairs, pairs.size()));
-            RC(upload(g.d_pairs, pairs.data(), pairs.size()));
-            RC(dalloc(&g.d_hot4, hot4.size()));
-            RC(upload(g.d_hot4, hot4.data(), hot4.size()));
-            RC(dalloc(&g.d_leaf9, leaf9.size()));
-            RC(upload(g.d_leaf9, leaf9.data(), leaf9.size()));
+            RC(dalloc(&gp->d_pairs, pairs.size()));
+            RC(upload(gp->d_pairs, pairs.data(), pairs.size()));
+            RC(dalloc(&gp->d_hot4, hot4.size()));
+            RC(upload(gp->d_hot4, hot4.data(), hot4.size()));
+            RC(dalloc(&gp->d_leaf9, leaf9.size()));
+            RC(upload(gp->d_leaf9, leaf9.data(), leaf9.size()));
         }
     }
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
@@ -2155,55 +2513,55 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
             total += (size_t)t.width * t.height;
         }
         if (total > (size_t)INT32_MAX) return fail(PT_E_UNSUPPORTED, "texture data too large");
-        RC(dalloc(&g.d_texels, total));
-        RC(dalloc(&g.d_texinfo, info.size()));
+        RC(dalloc(&gp->d_texels, total));
+        RC(dalloc(&gp->d_texinfo, info.size()));
         for (int i = 0; i < s->num_textures; ++i) {
             const pt_texture& t = s->textures[i];
-            HIPCHK(smemcpy(g.d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
+            HIPCHK(smemcpy(gp->d_texels + info[i].x, t.data, (size_t)t.width * t.height * 4, hipMemcpyHostToDevice));
         }
-        RC(upload(g.d_texinfo, info.data(), info.size()));
+        RC(upload(gp->d_texinfo, info.data(), info.size()));
         num_tex = s->num_textures;
     }
-    RC(dalloc(&g.d_image, (size_t)g.pixels_total * 3));
-    HIPCHK(smemset(g.d_image, 0, sizeof(float) * 3 * (size_t)g.pixels_total));
-    RC(dalloc(&g.d_ctl, 1));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
-    g.key_bits = 1;
-    while ((1 << g.key_bits) < std::max(2, s->num_materials)) g.key_bits++;
+    RC(dalloc(&gp->d_image, (size_t)gp->pixels_total * 3));
+    HIPCHK(smemset(gp->d_image, 0, sizeof(float) * 3 * (size_t)gp->pixels_total));
+    RC(dalloc(&gp->d_ctl, 1));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    gp->key_bits = 1;
+    while ((1 << gp->key_bits) < std::max(2, s->num_materials)) gp->key_bits++;
 
-    SceneDev& sc = g.sc;
-    sc.geoms = g.d_geoms;
-    sc.cull = g.d_cull;
-    sc.mats = g.d_mats;
-    sc.nodes = g.d_nodes;
-    sc.node_aux = g.d_node_aux;
-    sc.hot = g.d_hot;
-    sc.cold = g.d_cold;
+    SceneDev& sc = gp->sc;
+    sc.geoms = gp->d_geoms;
+    sc.cull = gp->d_cull;
+    sc.mats = gp->d_mats;
+    sc.nodes = gp->d_nodes;
+    sc.node_aux = gp->d_node_aux;
+    sc.hot = gp->d_hot;
+    sc.cold = gp->d_cold;
     sc.num_geoms = s->num_geoms;
     sc.num_mats = s->num_materials;
-    sc.num_nodes = g.has_bvh ? s->num_bvh_nodes : 0;
+    sc.num_nodes = gp->has_bvh ? s->num_bvh_nodes : 0;
     sc.num_tris = s->num_triangles;
     sc.trace_depth = s->trace_depth;
     sc.arg_order = o.arg_order;
-    sc.use_bvh = g.has_bvh ? 1 : 0;
-    sc.stack_depth = g.stack_depth;
+    sc.use_bvh = gp->has_bvh ? 1 : 0;
+    sc.stack_depth = gp->stack_depth;
     // the pair traversal pushes at most one entry per level of its hierarchy (never more than the
     // stack_depth the other traversals size their stacks for); k_bvh_bounce's LDS stack is sized
     // by it -- unless k_bvh_bounce walks the 4-wide layout, which needs stack_depth
-    sc.pair_stack_depth = g.pair_depth > 0 ? std::min(g.pair_depth, g.stack_depth) : g.stack_depth;
-    if (g.d_quads) sc.pair_stack_depth = g.stack_depth;
+    sc.pair_stack_depth = gp->pair_depth > 0 ? std::min(gp->pair_depth, gp->stack_depth) : gp->stack_depth;
+    if (gp->d_quads) sc.pair_stack_depth = gp->stack_depth;
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
-    sc.contrib = g.d_contrib;
-    sc.texels = g.d_texels;
-    sc.texinfo = g.d_texinfo;
+    sc.contrib = gp->d_contrib;
+    sc.texels = gp->d_texels;
+    sc.texinfo = gp->d_texinfo;
     sc.num_textures = num_tex;
-    sc.pairs = g.d_pairs;
-    sc.quads = g.d_quads;
+    sc.pairs = gp->d_pairs;
+    sc.quads = gp->d_quads;
     sc.num_quads = quad_count;
     sc.qroot_ref = quad_root_ref;
-    sc.hot4 = g.d_hot4;
-    sc.leaf9 = g.d_leaf9;
+    sc.hot4 = gp->d_hot4;
+    sc.leaf9 = gp->d_leaf9;
     sc.num_pairs = pair_count;
     sc.root_ref = pair_root_ref;
     sc.root_lo = pair_root_lo;
@@ -2213,19 +2571,90 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
     sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
     sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
     RC(ensure_frames(1));            // one frame's wavefront now; larger passes grow it on first use
-    g.inited = true;
+    gp->inited = true;
     HIPCHK(hipDeviceSynchronize());
+    return PT_OK;
+}
+
+int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
+    if (!s) return fail(PT_E_INVALID, "scene is NULL");
+    pt_free();
+    pt_options o;
+    if (opts_in) o = *opts_in;
+    else pt_default_options(&o);
+    if (o.num_devices < 0 || o.num_devices > PT_MAX_DEVICES)
+        return fail(PT_E_INVALID, "num_devices must be 0 .. %d", PT_MAX_DEVICES);
+    if (o.num_devices <= 1) {
+        const int rc = init_one(s, o, 1);
+        if (rc != PT_OK) free_all();   // whatever was allocated before the failure
+        return rc;
+    }
+    const int n = o.num_devices;
+    if (o.shard_mode != PT_SHARD_NONE)
+        return fail(PT_E_INVALID, "num_devices > 1 splits the frame itself; shard_mode must be PT_SHARD_NONE");
+    if (o.combine != PT_COMBINE_PEER && o.combine != PT_COMBINE_RCCL) return fail(PT_E_INVALID, "bad combine");
+    const int H = s->camera.resolution.y, rows = std::max(1, o.shard_rows);
+    if (H > 0 && (H + rows - 1) / rows < n)
+        return fail(PT_E_INVALID, "%d shards but only %d row bands of %d rows", n, (H + rows - 1) / rows, rows);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_E_NODEVICE, "no HIP device visible");
+    for (int k = 0; k < n; ++k)
+        if (o.device_ids[k] < 0 || o.device_ids[k] >= ndev)
+            return fail(PT_E_INVALID, "device_ids[%d] = %d out of range (%d devices)", k, o.device_ids[k], ndev);
+    M.n = n;
+    M.combine = o.combine;
+    int rc = PT_OK;
+    for (int k = 0; k < n && rc == PT_OK; ++k) {
+        M.shard[k] = k == 0 ? &g_primary : new State();
+        pt_options ok = o;
+        ok.num_devices = 1;
+        ok.device = o.device_ids[k];
+        ok.shard_mode = PT_SHARD_PIXELS;
+        ok.shard_rank = k;
+        ok.shard_count = n;
+        ok.shard_rows = rows;
+        int share = 0;
+        for (int j = 0; j < n; ++j) share += o.device_ids[j] == o.device_ids[k];
+        ShardScope sc(M.shard[k]);
+        rc = init_one(s, ok, share);
+    }
+    if (rc == PT_OK) rc = multi_setup();
+    if (rc != PT_OK) {
+        const std::string err = g_err;
+        pt_free();
+        g_err = err;
+        return rc;
+    }
+    HIPCHK(hipSetDevice(g_primary.device));
     return PT_OK;
 }
 
 int32_t pt_set_camera(const pt_camera* c) {
     RC(need_init());
-    if (!c || c->resolution.x != g.width || c->resolution.y != g.height)
+    if (!c || c->resolution.x != gp->width || c->resolution.y != gp->height)
         return fail(PT_E_INVALID, "camera resolution must match pt_init");
-    CamDev nc = to_camdev(*c);
-    if (memcmp(&nc, &g.sc.cam, sizeof nc) != 0) {
-        g.sc.cam = nc;
-        release_graph();   // kernel arguments changed
+    const CamDev nc = to_camdev(*c);
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        if (memcmp(&nc, &gp->sc.cam, sizeof nc) != 0) {
+            HIPCHK(hipStreamSynchronize(gp->stream));   // a replayed pass may still hold the graph
+            gp->sc.cam = nc;
+            release_graph();   // kernel arguments changed
+        }
+    }
+    return PT_OK;
+}
+
+int32_t pt_set_trace_depth(int32_t depth) {
+    RC(need_init());
+    if (depth < 0 || depth > MAXB) return fail(PT_E_UNSUPPORTED, "trace depth %d not in 0 .. %d", depth, MAXB);
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        if (gp->sc.trace_depth != depth) {
+            HIPCHK(hipStreamSynchronize(gp->stream));
+            gp->sc.trace_depth = depth;
+            release_graph();   // the bounce count is baked into the captured passes
+        }
     }
     return PT_OK;
 }
@@ -2234,10 +2663,14 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     (void)frame;   // unused by the reference too (pathtrace.cu:639)
     RC(need_init());
     if (iteration <= 0) return fail(PT_E_INVALID, "iteration is 1-based (main.cpp:458), got %d", iteration);
-    RC(run_frame(iteration));
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        RC(run_frame(iteration));
+    }
+    RC(multi_combine());
     if (pbo) {
-        hipLaunchKernelGGL(k_to_pbo, dim3(nblocks(g.pixels_total)), dim3(BLOCK), 0, g.stream, g.d_image, pbo,
-                           g.pixels_total, iteration);
+        hipLaunchKernelGGL(k_to_pbo, dim3(nblocks(gp->pixels_total)), dim3(BLOCK), 0, gp->stream, gp->d_image, pbo,
+                           gp->pixels_total, iteration);
         HIPCHK(hipGetLastError());
     }
     if (host_image) {
@@ -2245,27 +2678,21 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new
         // one at the same address, and on MI355X the pageable copy runs at the pinned rate anyway
         // (tools/copy_probe.py: 7.68 MB in 0.145 ms either way)
-        const size_t bytes = sizeof(float) * 3 * (size_t)g.pixels_total;
-        HIPCHK(hipMemcpyAsync(host_image, g.d_image, bytes, hipMemcpyDeviceToHost, g.stream));
+        const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
+        HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
     }
-    HIPCHK(hipStreamSynchronize(g.stream));
-    if (g.traced_depth) {
-        // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770): the
-        // loop stops after bounce k when no path is left alive, or at traceDepth
-        int depth = std::max(1, g.sc.trace_depth);
-        if (g.opts.stream_compaction) {
-            std::vector<int> cnt((size_t)depth * NSEG * CNT_PAD);
-            HIPCHK(smemcpy(cnt.data(), &g.d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
-            for (int k = 1; k < depth; ++k) {
-                int64_t live = 0;
-                for (int q = 0; q < NSEG; ++q) live += cnt[((size_t)k * NSEG + q) * CNT_PAD];
-                if (live == 0) {
-                    depth = k;
-                    break;
-                }
-            }
+    HIPCHK(hipStreamSynchronize(gp->stream));
+    if (gp->traced_depth) {
+        // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770); with
+        // shards, the frame ran as long as its longest shard
+        int depth = 0;
+        for (int k = 0; k < nshards(); ++k) {
+            ShardScope sc(shard_ctx(k));
+            int d = 0;
+            RC(frame_depth(d));
+            depth = std::max(depth, d);
         }
-        *g.traced_depth = depth;
+        *gp->traced_depth = depth;
     }
     return PT_OK;
 }
@@ -2273,56 +2700,69 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
 int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     RC(need_init());
     if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
-    // passes of g.batch frames (bit-identical to frame-by-frame: k_combine keeps the order)
-    for (int i = 0; i < count;) {
-        const int f = pass_frames(count - i);
-        RC(run_pass(first_iteration + i, f));
-        i += f;
+    // passes of gp->batch frames (bit-identical to frame-by-frame: k_combine keeps the order);
+    // every shard's passes are queued before the combine, so the devices trace concurrently
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        for (int i = 0; i < count;) {
+            const int f = pass_frames(count - i);
+            RC(run_pass(first_iteration + i, f));
+            i += f;
+        }
     }
-    return PT_OK;
+    return count > 0 ? multi_combine() : PT_OK;
 }
 
 int32_t pt_prepare_frames(int32_t count) {
     RC(need_init());
     if (count < 0) return fail(PT_E_INVALID, "bad count");
-    RC(ensure_frames(count > 0 ? pass_frames(count) : 1));   // the largest pass of the run comes first
-    if (!g.opts.use_graph) return PT_OK;
-    // the pass sizes pt_trace_frames(., count) will replay
-    for (int i = 0; i < count;) {
-        const int f = pass_frames(count - i);
-        if (!g.graph_exec[f]) RC(build_graph(f));
-        i += f;
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        RC(ensure_frames(count > 0 ? pass_frames(count) : 1));   // the largest pass of the run comes first
+        if (!gp->opts.use_graph) continue;
+        // the pass sizes pt_trace_frames(., count) will replay
+        for (int i = 0; i < count;) {
+            const int f = pass_frames(count - i);
+            if (!gp->graph_exec[f]) RC(build_graph(f));
+            i += f;
+        }
     }
     return PT_OK;
 }
 
 int32_t pt_synchronize(void) {
     RC(need_init());
-    HIPCHK(hipStreamSynchronize(g.stream));
+    for (int k = nshards() - 1; k >= 0; --k) {
+        ShardScope sc(shard_ctx(k));
+        HIPCHK(hipStreamSynchronize(gp->stream));
+    }
     return PT_OK;
 }
 
 int32_t pt_get_image(float* host_out, int64_t n_floats) {
     RC(need_init());
-    if (!host_out || n_floats < (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image buffer too small");
-    HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(smemcpy(host_out, g.d_image, sizeof(float) * 3 * (size_t)g.pixels_total, hipMemcpyDeviceToHost));
+    if (!host_out || n_floats < (int64_t)gp->pixels_total * 3) return fail(PT_E_INVALID, "image buffer too small");
+    HIPCHK(hipStreamSynchronize(gp->stream));
+    HIPCHK(smemcpy(host_out, gp->d_image, sizeof(float) * 3 * (size_t)gp->pixels_total, hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
 int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
     RC(need_init());
-    HIPCHK(hipStreamSynchronize(g.stream));
-    if (device_ptr) *device_ptr = g.d_image;
-    if (n_floats) *n_floats = (int64_t)g.pixels_total * 3;
+    HIPCHK(hipStreamSynchronize(gp->stream));
+    if (device_ptr) *device_ptr = gp->d_image;
+    if (n_floats) *n_floats = (int64_t)gp->pixels_total * 3;
     return PT_OK;
 }
 
 int32_t pt_set_image(const float* host_in, int64_t n_floats) {
     RC(need_init());
-    if (!host_in || n_floats != (int64_t)g.pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
-    HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(smemcpy(g.d_image, host_in, sizeof(float) * (size_t)n_floats, hipMemcpyHostToDevice));
+    if (!host_in || n_floats != (int64_t)gp->pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
+    for (int k = 0; k < nshards(); ++k) {   // each shard keeps accumulating into its own pixels of it
+        ShardScope sc(shard_ctx(k));
+        HIPCHK(hipStreamSynchronize(gp->stream));
+        HIPCHK(smemcpy(gp->d_image, host_in, sizeof(float) * (size_t)n_floats, hipMemcpyHostToDevice));
+    }
     return PT_OK;
 }
 
@@ -2343,24 +2783,46 @@ int32_t pt_device_free(void* p) {
 
 int32_t pt_device_read(void* host_dst, const void* device_src, int64_t bytes) {
     if (!host_dst || !device_src || bytes < 0) return fail(PT_E_INVALID, "pt_device_read: bad argument");
-    if (g.stream) HIPCHK(hipStreamSynchronize(g.stream));
+    if (gp->stream) HIPCHK(hipStreamSynchronize(gp->stream));
     HIPCHK(smemcpy(host_dst, device_src, (size_t)bytes, hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
+static int32_t frame_stats(pt_frame_stats* out);   // the current context's (below)
+
 int32_t pt_get_frame_stats(pt_frame_stats* out) {
     RC(need_init());
     if (!out) return fail(PT_E_INVALID, "NULL");
-    HIPCHK(hipStreamSynchronize(g.stream));
+    RC(frame_stats(out));
+    for (int k = 1; k < nshards(); ++k) {   // shards: the counts of every shard's pixels
+        pt_frame_stats s;
+        {
+            ShardScope sc(shard_ctx(k));
+            RC(frame_stats(&s));
+        }
+        out->pixels += s.pixels;
+        out->segments += s.segments;
+        out->segments_total += s.segments_total;
+        for (int b = 0; b < 64; ++b) out->live[b] += s.live[b];
+        for (int b = 0; b <= MAXB; ++b) {
+            out->live_total[b] += s.live_total[b];
+            out->queued_total[b] += s.queued_total[b];
+        }
+    }
+    return PT_OK;
+}
+
+static int32_t frame_stats(pt_frame_stats* out) {
+    HIPCHK(hipStreamSynchronize(gp->stream));
     FrameCtl ctl;
-    HIPCHK(smemcpy(&ctl, g.d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(&ctl, gp->d_ctl, sizeof ctl, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof(*out));
     out->iteration = ctl.iter;
-    out->bounces = std::max(1, g.sc.trace_depth);
-    out->pixels = g.local_pixels;
+    out->bounces = std::max(1, gp->sc.trace_depth);
+    out->pixels = gp->local_pixels;
     for (int b = 0; b < out->bounces; ++b) {
         int64_t s = 0;
-        if (g.opts.pipeline == PT_PIPELINE_STAGED && !g.opts.stream_compaction) {
+        if (gp->opts.pipeline == PT_PIPELINE_STAGED && !gp->opts.stream_compaction) {
             s = b == 0 ? ctl.cnt[0][0][0] : -1;   // no compaction: the live count is never formed
         } else {
             for (int k = 0; k < NSEG; ++k) s += ctl.cnt[b][k][0];
@@ -2369,7 +2831,7 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
         if (s > 0) out->segments += s;
     }
     out->frames_total = (int64_t)ctl.frames;
-    out->frames_per_pass = g.batch;
+    out->frames_per_pass = gp->batch;
     out->last_pass_frames = ctl.batch;
     for (int b = 0; b <= MAXB; ++b) {
         int64_t cur = 0;
@@ -2383,8 +2845,11 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
 
 int32_t pt_reset_stats(void) {
     RC(need_init());
-    HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        HIPCHK(hipStreamSynchronize(gp->stream));
+        HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    }
     return PT_OK;
 }
 
@@ -2393,21 +2858,23 @@ int32_t pt_reset_stats(void) {
 // ---------------------------------------------------------------------------------------------
 int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(need_init());
-    if (!out || n < g.local_pixels) return fail(PT_E_INVALID, "output too small");
+    RC(need_single("pt_test_camera"));
+    if (!out || n < gp->local_pixels) return fail(PT_E_INVALID, "output too small");
     RC(ensure_frames(1));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
-    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, g.stream, g.d_ctl, iteration, g.local_pixels, 1);
-    hipLaunchKernelGGL(k_camera, dim3(nblocks(g.local_pixels)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), g.d_ctl);
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, gp->stream, gp->d_ctl, iteration, gp->local_pixels, 1);
+    hipLaunchKernelGGL(k_camera, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->stream, gp->sc, pathbuf(0), gp->d_ctl);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     release_graph();
-    RC(download_paths(0, g.local_pixels, out));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    RC(download_paths(0, gp->local_pixels, out));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
 int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_isect* isects) {
     RC(need_init());
+    RC(need_single("pt_test_intersect"));
     RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
@@ -2422,29 +2889,29 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
                 if (x) (void)hipFree(x);
         }
     } tmp;
-    float4 *uvd0 = g.d_hit_uvd0, *uvd1 = g.d_hit_uvd1;
-    if (!uvd0 && g.has_bvh) {
+    float4 *uvd0 = gp->d_hit_uvd0, *uvd1 = gp->d_hit_uvd1;
+    if (!uvd0 && gp->has_bvh) {
         RC(dalloc(&tmp.p[0], (size_t)n));
         RC(dalloc(&tmp.p[1], (size_t)n));
         uvd0 = tmp.p[0];
         uvd1 = tmp.p[1];
     }
-    HitBuf hits{g.d_hit_nt, g.d_hit_mat, uvd0, uvd1};
-    if (g.has_bvh && (g.opts.variant & VAR_BVH_FAST))
-        hipLaunchKernelGGL((k_intersect<true, true>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
+    HitBuf hits{gp->d_hit_nt, gp->d_hit_mat, uvd0, uvd1};
+    if (gp->has_bvh && (gp->opts.variant & VAR_BVH_FAST))
+        hipLaunchKernelGGL((k_intersect<true, true>), dim3(nblocks((int)n)), dim3(BLOCK), gp->bvh_lds, gp->stream, gp->sc,
                            pathbuf(0), hits, staged_count(0));
-    else if (g.has_bvh)
-        hipLaunchKernelGGL((k_intersect<true, false>), dim3(nblocks((int)n)), dim3(BLOCK), g.bvh_lds, g.stream, g.sc,
+    else if (gp->has_bvh)
+        hipLaunchKernelGGL((k_intersect<true, false>), dim3(nblocks((int)n)), dim3(BLOCK), gp->bvh_lds, gp->stream, gp->sc,
                            pathbuf(0), hits, staged_count(0));
     else
-        hipLaunchKernelGGL((k_intersect<false, false>), dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc,
+        hipLaunchKernelGGL((k_intersect<false, false>), dim3(nblocks((int)n)), dim3(BLOCK), 0, gp->stream, gp->sc,
                            pathbuf(0), hits, staged_count(0));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     std::vector<float4> nt(n);
     std::vector<int> mat(n);
-    HIPCHK(smemcpy(nt.data(), g.d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
-    HIPCHK(smemcpy(mat.data(), g.d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(nt.data(), gp->d_hit_nt, n * sizeof(float4), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(mat.data(), gp->d_hit_mat, n * sizeof(int), hipMemcpyDeviceToHost));
     std::vector<float4> a0, a1;
     if (uvd0) {
         a0.resize(n);
@@ -2464,12 +2931,13 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
         }
     }
     release_graph();
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
 int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_path_segment* paths, int64_t n) {
     RC(need_init());
+    RC(need_single("pt_test_shade"));
     RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
     RC(upload_paths(0, paths, n));
@@ -2480,79 +2948,81 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
         nt[i] = make_float4(isects[i].surfaceNormal.x, isects[i].surfaceNormal.y, isects[i].surfaceNormal.z,
                             isects[i].t);
         mat[i] = isects[i].materialId;
-        if (isects[i].t > 0.0f && (mat[i] < 0 || mat[i] >= std::max(1, g.sc.num_mats)))
+        if (isects[i].t > 0.0f && (mat[i] < 0 || mat[i] >= std::max(1, gp->sc.num_mats)))
             return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
     }
-    HIPCHK(smemcpy(g.d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHK(smemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    if (g.d_hit_uvd0) {
+    HIPCHK(smemcpy(gp->d_hit_nt, nt.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(gp->d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    if (gp->d_hit_uvd0) {
         std::vector<float4> a0(n), a1(n);
         for (int64_t i = 0; i < n; ++i) {
             const pt_shadeable_isect& x = isects[i];
             a0[i] = make_float4(x.uv.x, x.uv.y, x.dpdu.x, x.dpdu.y);
             a1[i] = make_float4(x.dpdu.z, x.dpdv.x, x.dpdv.y, x.dpdv.z);
         }
-        HIPCHK(smemcpy(g.d_hit_uvd0, a0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
-        HIPCHK(smemcpy(g.d_hit_uvd1, a1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(smemcpy(gp->d_hit_uvd0, a0.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHK(smemcpy(gp->d_hit_uvd1, a1.data(), n * sizeof(float4), hipMemcpyHostToDevice));
     }
-    HitBuf hits{g.d_hit_nt, g.d_hit_mat, g.d_hit_uvd0, g.d_hit_uvd1};
-    hipLaunchKernelGGL(k_shade, dim3(nblocks((int)n)), dim3(BLOCK), 0, g.stream, g.sc, pathbuf(0), hits,
-                       (const int*)nullptr, staged_count(0), (const FrameCtl*)g.d_ctl, iteration, (float*)nullptr,
+    HitBuf hits{gp->d_hit_nt, gp->d_hit_mat, gp->d_hit_uvd0, gp->d_hit_uvd1};
+    hipLaunchKernelGGL(k_shade, dim3(nblocks((int)n)), dim3(BLOCK), 0, gp->stream, gp->sc, pathbuf(0), hits,
+                       (const int*)nullptr, staged_count(0), (const FrameCtl*)gp->d_ctl, iteration, (float*)nullptr,
                        (int*)nullptr);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     release_graph();
     RC(download_paths(0, n, paths));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
 int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment* out, int64_t* alive_out) {
     RC(need_init());
+    RC(need_single("pt_test_compact"));
     RC(ensure_test_paths(n));
     RC(upload_paths(0, paths, n));
     std::vector<int> al(std::max<int64_t>(1, n));
     for (int64_t i = 0; i < n; ++i) al[i] = paths[i].remainingBounces > 0;   // PathAlive
-    if (n) HIPCHK(smemcpy(g.d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    if (n) HIPCHK(smemcpy(gp->d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     RC(set_count(0, (int)n));
     if (n > 0) {   // the pipeline's launch sequence
-        launch_compact<CITEMS>(pathbuf(0), pathbuf(1), staged_count(0), &g.d_ctl->cnt[1][0][0], (int)n);
+        launch_compact<CITEMS>(pathbuf(0), pathbuf(1), staged_count(0), &gp->d_ctl->cnt[1][0][0], (int)n);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     int na = 0;
-    HIPCHK(smemcpy(&na, &g.d_ctl->cnt[1][0][0], sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(smemcpy(&na, &gp->d_ctl->cnt[1][0][0], sizeof(int), hipMemcpyDeviceToHost));
     if (alive_out) *alive_out = na;
     release_graph();
     RC(download_paths(1, na, out));
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
 int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm) {
     RC(need_init());
+    RC(need_single("pt_test_sort"));
     RC(ensure_test_paths(n));
     if (n == 0) return PT_OK;
-    const int nk = std::max(1, g.sc.num_mats);
+    const int nk = std::max(1, gp->sc.num_mats);
     std::vector<int> mat(n);
     for (int64_t i = 0; i < n; ++i) {
         mat[i] = isects[i].materialId;
         if (mat[i] < 0 || mat[i] >= nk) return fail(PT_E_INVALID, "materialId %d out of range", mat[i]);
     }
-    HIPCHK(smemcpy(g.d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(smemcpy(gp->d_hit_mat, mat.data(), n * sizeof(int), hipMemcpyHostToDevice));
     RC(set_count(0, (int)n));
     const int ntiles = (int)((n + STILE - 1) / STILE);
-    hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
-                       g.d_tile_hist);
-    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, g.stream, g.d_tile_hist, staged_count(0), nk);
-    hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, g.stream, g.d_hit_mat, staged_count(0), nk,
-                       g.key_bits, g.d_tile_hist, g.d_perm);
+    hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(BLOCK), 0, gp->stream, gp->d_hit_mat, staged_count(0), nk,
+                       gp->d_tile_hist);
+    hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(SCAN_THREADS), 0, gp->stream, gp->d_tile_hist, staged_count(0), nk);
+    hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(BLOCK), 0, gp->stream, gp->d_hit_mat, staged_count(0), nk,
+                       gp->key_bits, gp->d_tile_hist, gp->d_perm);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(g.stream));
-    HIPCHK(smemcpy(perm, g.d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipStreamSynchronize(gp->stream));
+    HIPCHK(smemcpy(perm, gp->d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
     release_graph();
-    HIPCHK(smemset(g.d_ctl, 0, sizeof(FrameCtl)));
+    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
     return PT_OK;
 }
 
@@ -2594,21 +3064,22 @@ int32_t pt_test_pbo(const float* image, int64_t n, int32_t iteration, pt_uchar4*
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset) {
     RC(need_init());
     if (!out || n < 0 || n > SEC_SLOTS) return fail(PT_E_INVALID, "bad arguments");
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     unsigned long long tmp[SEC_SLOTS];
-    HIPCHK(hipMemcpyFromSymbolAsync(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost, g.stream));
-    HIPCHK(hipStreamSynchronize(g.stream));
+    HIPCHK(hipMemcpyFromSymbolAsync(tmp, HIP_SYMBOL(g_sections), sizeof tmp, 0, hipMemcpyDeviceToHost, gp->stream));
+    HIPCHK(hipStreamSynchronize(gp->stream));
     for (int i = 0; i < n; ++i) out[i] = tmp[i];
     if (reset) {
         memset(tmp, 0, sizeof tmp);
-        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sections), tmp, sizeof tmp, 0, hipMemcpyHostToDevice, g.stream));
-        HIPCHK(hipStreamSynchronize(g.stream));
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sections), tmp, sizeof tmp, 0, hipMemcpyHostToDevice, gp->stream));
+        HIPCHK(hipStreamSynchronize(gp->stream));
     }
     return PT_OK;
 }
 
 int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_times* out) {
     RC(need_init());
+    RC(need_single("pt_profile_frames"));
     if (!out || count <= 0) return fail(PT_E_INVALID, "bad arguments");
     memset(out, 0, sizeof(*out));
     RC(ensure_frames(pass_frames(count)));
@@ -2620,8 +3091,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     {   // every kernel of every pass gets a start and a stop event, created up front
-        const int passes = (count + g.batch - 1) / g.batch;
-        const size_t need = 2 * (size_t)passes * (size_t)(4 * std::max(1, g.sc.trace_depth) + 8);
+        const int passes = (count + gp->batch - 1) / gp->batch;
+        const size_t need = 2 * (size_t)passes * (size_t)(4 * std::max(1, gp->sc.trace_depth) + 8);
         while (g_prof_pool.size() < need) {
             hipEvent_t e = nullptr;
             HIPCHK(hipEventCreateWithFlags(&e, PROF_EVENT_FLAGS));
@@ -2629,20 +3100,20 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
         }
         g_prof_next = 0;
     }
-    HIPCHK(hipEventRecord(e0, g.stream));
+    HIPCHK(hipEventRecord(e0, gp->stream));
     g_prof = &rec;
     int rc = PT_OK;
     for (int i = 0; i < count && rc == PT_OK;) {
         const int f = pass_frames(count - i);
         pass_start.push_back(rec.size());
         rc = enqueue_pass(first_iteration + i, f);
-        g.frames_done += f;
-        g.last_iter = first_iteration + i + f - 1;
+        gp->frames_done += f;
+        gp->last_iter = first_iteration + i + f - 1;
         i += f;
     }
     g_prof = nullptr;
-    (void)hipEventRecord(e1, g.stream);
-    hipError_t se = hipStreamSynchronize(g.stream);
+    (void)hipEventRecord(e1, gp->stream);
+    hipError_t se = hipStreamSynchronize(gp->stream);
     const int passes = (int)pass_start.size();
     double bounce_ms[MAXB] = {0}, bvh_ms[MAXB] = {0};
     double compact_ms = 0, isect_ms = 0, shade_ms = 0, cam_ms = 0, sort_ms = 0, scan_ms = 0, comb_ms = 0, tail_ms = 0;

@@ -15,7 +15,7 @@
 // The reference's Scene vectors are handed over without a copy: their element types have the
 // byte layout of the pt_* records (checked below, and field by field against sceneStructs.h in
 // tests/test_ref_pins.py::test_struct_layout_matches_reference).  Behaviour follows pathtrace.cu:
-// a non-owning Scene*, the camera re-read on every frame, scene->state.image overwritten with the
+// a non-owning Scene*, the trace depth and the camera re-read on every frame, scene->state.image overwritten with the
 // accumulated image on every frame, and on any error a message then exit(EXIT_FAILURE)
 // (checkCUDAErrorFn, pathtrace.cu:27-49).
 #include "pathtrace.h"
@@ -80,7 +80,8 @@ void pathtraceFree() { PT_CHECK(pt_free(), "pathtraceFree"); }
 
 void pathtrace(uchar4* pbo, int frame, int iteration) {
     if (!hst_scene) PT_CHECK(PT_E_STATE, "pathtrace before pathtraceInit");
-    // the camera is re-read from the Scene every frame (pathtrace.cu:642)
+    // the trace depth and the camera are re-read from the Scene every frame (pathtrace.cu:641-642)
+    PT_CHECK(pt_set_trace_depth(hst_scene->state.traceDepth), "pathtrace traceDepth");
     PT_CHECK(pt_set_camera(reinterpret_cast<const pt_camera*>(&hst_scene->state.camera)), "pathtrace camera");
     float* img = hst_scene->state.image.empty() ? nullptr : &hst_scene->state.image[0].x;
     PT_CHECK(pt_trace(reinterpret_cast<pt_uchar4*>(pbo), frame, iteration, img), "pathtrace");

@@ -38,7 +38,8 @@ void pathtraceFree() { check(pt_free(), "pathtraceFree"); }
 
 void pathtrace(uchar4* pbo, int frame, int iteration) {
     if (!hst_scene) check(PT_E_STATE, "pathtrace before pathtraceInit");
-    // the reference re-reads the camera from the Scene every frame (pathtrace.cu:642)
+    // the reference re-reads the trace depth and the camera from the Scene every frame (pathtrace.cu:641-642)
+    check(pt_set_trace_depth(hst_scene->state.traceDepth), "pathtrace traceDepth");
     check(pt_set_camera(&hst_scene->state.camera), "pathtrace camera");
     float* img = hst_scene->state.image.empty() ? nullptr : &hst_scene->state.image[0].x;
     check(pt_trace(pbo, frame, iteration, img), "pathtrace");

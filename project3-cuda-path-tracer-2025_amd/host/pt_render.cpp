@@ -6,6 +6,7 @@
 //
 //   pt_render SCENE.json [--spp N] [--res WxH] [--depth D] [--out PREFIX]
 //             [--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K] [--gpu-bvh]
+//             [--devices N | --devices K0,K1,...] [--combine peer|rccl]
 //             [--events FILE [--img-dir DIR] [--time-tag TAG]]
 //
 // --events replays a recorded window session through the viewer state machine of
@@ -18,6 +19,7 @@
 //   display FILE.png  write the window's pixels (the PBO as mainLoop draws it)
 // The session ends at the end of the file, on ESC (window closed) or when runCuda reaches
 // ITERATIONS (image saved, process exits), like the reference's main loop.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -108,6 +110,7 @@ int main(int argc, char** argv) {
     if (argc < 2) {
         std::printf("Usage: %s SCENEFILE.json [--spp N] [--res WxH] [--depth D] [--out PREFIX] "
                     "[--pipeline fused|staged] [--sort] [--no-compaction] [--no-bvh] [--device K] [--gpu-bvh] "
+                    "[--devices N|K0,K1,... [--combine peer|rccl]] "
                     "[--events FILE [--img-dir DIR] [--time-tag TAG]]\n", argv[0]);
         return 1;
     }
@@ -132,6 +135,20 @@ int main(int argc, char** argv) {
         else if (a == "--no-bvh") opts.bvh = 0;
         else if (a == "--device") opts.device = std::atoi(next());
         else if (a == "--gpu-bvh") gpu_bvh = true;
+        else if (a == "--devices") {   // every frame split into pixel shards over these GPUs
+            const std::string d = next();
+            opts.num_devices = 0;
+            if (d.find(',') == std::string::npos) {
+                opts.num_devices = std::max(0, std::min(PT_MAX_DEVICES, std::atoi(d.c_str())));
+                for (int k = 0; k < PT_MAX_DEVICES; ++k) opts.device_ids[k] = k;
+            } else {
+                for (size_t s = 0; s <= d.size() && opts.num_devices < PT_MAX_DEVICES;) {
+                    const size_t e = std::min(d.find(',', s), d.size());
+                    opts.device_ids[opts.num_devices++] = std::atoi(d.substr(s, e - s).c_str());
+                    s = e + 1;
+                }
+            }
+        } else if (a == "--combine") opts.combine = std::strcmp(next(), "rccl") == 0 ? PT_COMBINE_RCCL : PT_COMBINE_PEER;
         else if (a == "--events") events = next();
         else if (a == "--img-dir") img_dir = next();
         else if (a == "--time-tag") time_tag = next();

@@ -47,6 +47,8 @@ ISECT = np.dtype([("t", "<f4"), ("surfaceNormal", "<f4", (3,)), ("materialId", "
 PT_OK = 0
 PIPELINE_FUSED, PIPELINE_STAGED = 0, 1
 SHARD_NONE, SHARD_PIXELS, SHARD_SAMPLES = 0, 1, 2
+COMBINE_PEER, COMBINE_RCCL = 0, 1
+MAX_DEVICES = 16
 
 
 class PtError(RuntimeError):
@@ -56,7 +58,8 @@ class PtError(RuntimeError):
 class _Options(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "stream_compaction", "material_sort", "bvh", "arg_order", "pipeline", "use_graph", "device",
-        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size", "variant", "frames_per_pass")]
+        "shard_mode", "shard_rank", "shard_count", "shard_rows", "block_size", "variant", "frames_per_pass",
+        "num_devices")] + [("device_ids", ctypes.c_int32 * MAX_DEVICES), ("combine", ctypes.c_int32)]
 
 
 class _SceneView(ctypes.Structure):
@@ -94,7 +97,7 @@ ABI_SYMBOLS = [
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
     "pt_save_png", "pt_scene_load_ex", "pt_bvh_build", "pt_bvh_build_last_error", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
-    "pt_device_alloc", "pt_device_free", "pt_device_read",
+    "pt_device_alloc", "pt_device_free", "pt_device_read", "pt_set_trace_depth",
 ]
 # include/pt/pt_viewer.h (the headless interactive viewer)
 VIEWER_SYMBOLS = [
@@ -131,6 +134,7 @@ def _load():
         "pt_scene_load_ex": (i32, [ctypes.c_char_p, i32, i32, i32, i32, vp]),
         "pt_bvh_build": (i32, [vp, i32, vp, i32, vp, vp]),
         "pt_bvh_build_last_error": (ctypes.c_char_p, []),
+        "pt_set_trace_depth": (i32, [i32]),
         "pt_device_alloc": (i32, [i64, vp]), "pt_device_free": (i32, [vp]), "pt_device_read": (i32, [vp, vp, i64]),
         "pt_viewer_create": (i32, [vp, vp, ctypes.c_char_p, ctypes.c_char_p, vp]), "pt_viewer_destroy": (None, [vp]),
         "pt_viewer_mouse_button": (i32, [vp, i32, i32, i32]),
@@ -160,10 +164,22 @@ def _ptr(a):
 
 
 def default_options(**kw) -> _Options:
+    """pt_options with overrides.  `devices=[0, 0, 1]` traces every frame as one pixel shard per
+    entry on those GPUs (pt_options.num_devices / device_ids); `combine="peer"|"rccl"`."""
     o = _Options()
     lib.pt_default_options(ctypes.byref(o))
+    devices = kw.pop("devices", None)
+    if devices is not None:
+        devices = list(devices)
+        if len(devices) > MAX_DEVICES:
+            raise ValueError(f"at most {MAX_DEVICES} devices")
+        o.num_devices = len(devices)
+        for i, d in enumerate(devices):
+            o.device_ids[i] = int(d)
+    if isinstance(kw.get("combine"), str):
+        kw["combine"] = {"peer": COMBINE_PEER, "rccl": COMBINE_RCCL}[kw["combine"]]
     for k, v in kw.items():
-        if not hasattr(o, k):
+        if not hasattr(o, k) or k == "device_ids":
             raise TypeError(f"unknown option {k}")
         setattr(o, k, int(v))
     return o
@@ -311,6 +327,11 @@ class PathTracer:
             img = self._host_image
         _check(lib.pt_trace(pbo_device_ptr, 0, self.iteration, _ptr(img)), "pt_trace")
         return img
+
+    def set_trace_depth(self, depth: int):
+        """RenderState::traceDepth for the next frames (re-read per pathtrace call, pathtrace.cu:641)."""
+        _check(lib.pt_set_trace_depth(int(depth)), "pt_set_trace_depth")
+        self.trace_depth = int(depth)
 
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")

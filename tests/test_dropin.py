@@ -30,7 +30,7 @@ def test_dropin_exports_the_reference_signatures():
                 "_Z9pathtraceP6uchar4ii"):
         assert sym in defined, sym
     undefined = {l.split()[-1] for l in out.splitlines() if " U " in l}
-    assert {"pt_init", "pt_trace", "pt_free", "pt_set_camera", "pt_init_data_container"} <= undefined
+    assert {"pt_init", "pt_trace", "pt_free", "pt_set_camera", "pt_init_data_container", "pt_set_trace_depth"} <= undefined
 
 
 @needs_exe
@@ -70,6 +70,48 @@ def test_dropin_frames_bitexact(name, res, frames, tmp_path, oracle):
     sc = oracle.load_scene(path)
     r = oracle.Renderer(sc, oracle.options(trig_mode=1, arg_order=0))
     for it in range(1, frames + 1):
+        live = r.trace(it)
+    assert got.tobytes() == r.image.tobytes(), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
+    ran = next((k for k in range(1, sc.trace_depth) if live[k] <= 0), sc.trace_depth)
+    assert f"traced_depth {ran}" in p.stdout
+
+
+@needs_exe
+@pytest.mark.gpu
+def test_dropin_rereads_trace_depth_every_frame(tmp_path, oracle):
+    """pathtrace.cu:641 reads state.traceDepth at every call: a caller that lowers it before frame 2
+    gets frames 2.. at the new depth (oracle traced the same way), bit for bit."""
+    path = _small_scene(tmp_path, "cornell", (48, 48))
+    out = tmp_path / "img.f32"
+    p = subprocess.run([EXE, path, "3", str(out), "2:3"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = np.fromfile(out, np.float32).reshape(-1, 3)
+    sc = oracle.load_scene(path)
+    r = oracle.Renderer(sc, oracle.options(trig_mode=1, arg_order=0))
+    r.trace(1)
+    sc.trace_depth = r.cs.trace_depth = 3
+    for it in (2, 3):
+        live = r.trace(it)
+    assert got.tobytes() == r.image.tobytes(), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
+    ran = next((k for k in range(1, 3) if live[k] <= 0), 3)
+    assert f"traced_depth {ran}" in p.stdout
+
+
+@needs_exe
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,combine", [("0,0", "peer"), ("0,0,0", "rccl")])
+def test_dropin_several_device_shards(devices, combine, tmp_path, oracle):
+    """the reference's caller reaches the multi-device frame split through the environment
+    (PT_DEVICES / PT_COMBINE, read by pt_default_options): same image, same TracedDepth."""
+    path = _small_scene(tmp_path, "cornell_obj_bnnuy", (48, 48))
+    out = tmp_path / "img.f32"
+    env = dict(os.environ, PT_DEVICES=devices, PT_COMBINE=combine)
+    p = subprocess.run([EXE, path, "2", str(out)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = np.fromfile(out, np.float32).reshape(-1, 3)
+    sc = oracle.load_scene(path)
+    r = oracle.Renderer(sc, oracle.options(trig_mode=1, arg_order=0))
+    for it in (1, 2):
         live = r.trace(it)
     assert got.tobytes() == r.image.tobytes(), int(np.sum(got.view(np.uint32) != r.image.view(np.uint32)))
     ran = next((k for k in range(1, sc.trace_depth) if live[k] <= 0), sc.trace_depth)
