@@ -9,6 +9,7 @@ grouping of the geoms' boxes.  Waves either in path order or after regrouping ea
 by the ray direction's dominant axis (6 classes).
 
     python tools/cluster_study.py [--scene cornell_obj_khaslana] [--res 160] [--frames 2]
+    python tools/cluster_study.py --tree [...]     # per-lane tree over the geoms' boxes (below)
 """
 import argparse
 import os
@@ -101,5 +102,103 @@ def main():
                   f"clustered {clus / waves:.1f} ({clus / flat:.2f}x)")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--tree" not in sys.argv:
     main()
+
+
+# ---------------------------------------------------------------------------------------------
+# a per-lane tree over the geoms' boxes instead of the flat pre-test.
+# Each lane walks its own binary tree (near-first is irrelevant without a t bound: the pre-test
+# has no exact hit to cull with, so a lane visits every node its infinite ray passes); the wave
+# runs as long as its slowest lane.  Counted: node (box) tests per lane, the wave-max per wave,
+# for a tree over all geoms and for "large boxes flat + tree over the rest".
+# ---------------------------------------------------------------------------------------------
+def sah_tree(lo, hi, ids):
+    """binary SAH tree (object split over centroid-sorted prefixes) -> nested tuples"""
+    if len(ids) == 1:
+        return ids[0]
+    def area(l, h):
+        e = np.maximum(h - l, 0)
+        return e[0] * e[1] + e[1] * e[2] + e[2] * e[0]
+    best = None
+    for ax in range(3):
+        order = sorted(ids, key=lambda i: lo[i][ax] + hi[i][ax])
+        for s in range(1, len(order)):
+            L, R = order[:s], order[s:]
+            c = (area(lo[L].min(0), hi[L].max(0)) * len(L) + area(lo[R].min(0), hi[R].max(0)) * len(R))
+            if best is None or c < best[0]:
+                best = (c, L, R)
+    return (sah_tree(lo, hi, best[1]), sah_tree(lo, hi, best[2]))
+
+
+def tree_boxes(t, lo, hi, out):
+    if isinstance(t, tuple):
+        a = tree_boxes(t[0], lo, hi, out)
+        b = tree_boxes(t[1], lo, hi, out)
+        box = (np.minimum(a[0], b[0]), np.maximum(a[1], b[1]))
+    else:
+        box = (lo[t], hi[t])
+    out.append((t, box))
+    return box
+
+
+def lane_visits(t, o, d, lo, hi):
+    """node tests per ray of a per-lane DFS of tree t (every node whose box the ray passes)"""
+    nodes = []
+    tree_boxes(t, lo, hi, nodes)
+    box_of = {id(n): b for n, b in nodes}
+    visits = np.zeros(len(o), np.int64)
+    def walk(n, mask):
+        # mask: rays that reached node n (the parent's box passed): they test n's box
+        visits[mask] += 1
+        l, h = box_of[id(n)] if isinstance(n, tuple) else (lo[n], hi[n])
+        p = np.zeros(len(o), bool)
+        p[mask] = passes(o[mask], d[mask], l[None], h[None])[:, 0]
+        if isinstance(n, tuple) and p.any():
+            walk(n[0], p)
+            walk(n[1], p)
+    walk(t, np.ones(len(o), bool))
+    return visits
+
+
+def tree_study(sc, rays, lo, hi):
+    ng = len(lo)
+    ext = (hi - lo).max(1)
+    big = [i for i in range(ng) if ext[i] > 0.5 * ext.max()]
+    rest = [i for i in range(ng) if i not in big]
+    o = np.concatenate([x for x, _ in rays])
+    d = np.concatenate([y for _, y in rays])
+    full = sah_tree(lo, hi, list(range(ng)))
+    part = sah_tree(lo, hi, rest) if len(rest) > 1 else None
+    v_full = lane_visits(full, o, d, lo, hi)
+    v_part = len(big) + (lane_visits(part, o, d, lo, hi) if part is not None else 0)
+    cand = passes(o, d, lo, hi).sum(1)
+    for name, v in (("tree over all geoms", v_full), (f"{len(big)} large flat + tree over {len(rest)}", v_part)):
+        wmax = [v[w:w + 64].max() for w in range(0, len(v), 64)]
+        print(f"  {name}: box tests per lane mean {v.mean():.1f}, wave-max mean {np.mean(wmax):.1f} "
+              f"(flat: {ng} per lane; boxes passed per ray {cand.mean():.2f})")
+
+
+def tree_main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="cornell_obj_khaslana")
+    ap.add_argument("--res", type=int, default=160)
+    ap.add_argument("--frames", type=int, default=2)
+    args, _ = ap.parse_known_args()
+    sc = O.load_scene(os.path.join(REPO, "scenes", args.scene + ".json"), res=(args.res, args.res))
+    lo, hi = world_boxes(sc)
+    rays = []
+    r = O.Renderer(sc, O.options(trig_mode=1))
+    for it in range(1, args.frames + 1):
+        _, dump = r.trace(it, dump=True)
+        for b in range(1, sc.trace_depth):
+            p = dump[b][dump[b]["remainingBounces"] > 0]
+            if len(p):
+                rays.append((p["origin"].astype(np.float64), p["direction"].astype(np.float64)))
+    print(f"{args.scene}: {len(lo)} geoms, {sum(len(o) for o, _ in rays)} bounce>=1 rays (per-lane tree study)")
+    tree_study(sc, rays, lo, hi)
+
+
+if __name__ == "__main__" and "--tree" in sys.argv:
+    sys.argv.remove("--tree")
+    tree_main()
