@@ -81,7 +81,24 @@ struct SceneDev {
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
+    // candidate table of the pre-test (scenes of GRID_MIN_GEOMS..64 geoms; null: flat pre-test):
+    // per (origin cell, direction bin) the geoms a ray from that cell in that cone can hit
+    const unsigned long long* grid;
+    unsigned long long grid_all;   // every geom (rays outside the table's domain)
+    float grid_lo[3], grid_inv[3]; // cell = floor((o - grid_lo) * grid_inv), GRID_G per axis
 };
+
+// The candidate table's resolution: GRID_G^3 origin cells x 6 faces x GRID_B^2 direction bins
+// (1.5 MB of 64-bit masks at 8 / 8)
+#ifndef PT_GRID_G
+#define PT_GRID_G 8
+#endif
+#ifndef PT_GRID_B
+#define PT_GRID_B 8
+#endif
+constexpr int GRID_G = PT_GRID_G;
+constexpr int GRID_B = PT_GRID_B;
+constexpr int GRID_MIN_GEOMS = 16;
 
 // frame control block (device memory); zeroed / advanced by k_frame_begin every frame
 struct FrameCtl {
@@ -850,6 +867,38 @@ PT_DEV float cull_entry(const DevGeom& g, const CullRay& c) {   // +inf: certain
                                      __builtin_fmaxf(a2, b2));
     return (t1 >= t0) ? t0 : __builtin_inff();
 }
+// The pre-test from the candidate table (sc.grid): the table gives each lane a superset of the
+// geoms its ray can hit at all -- built on the host (pt_init, build_candidate_table) by interval
+// arithmetic over every origin in the cell (grown by the cell computation's rounding) and every
+// direction in the bin (grown by the bin computation's rounding), against the same conservative
+// world boxes the pre-test uses, which contain every exact hit point.  Each lane then runs the
+// flat pre-test's arithmetic (cull_candidates, bit for bit) on its own superset only, reading the
+// records from the block's LDS copy (`lc`, 3 float4 per geom).  A geom outside the superset cannot
+// be hit, so the exact tests of the candidates that remain find the same first minimum.  Rays
+// whose origin lies outside the table or whose direction is not finite take every geom.
+PT_DEV uint64_t grid_superset(const SceneDev& sc, f3 ro, f3 rd) {
+    const float fx = (ro.x - sc.grid_lo[0]) * sc.grid_inv[0];
+    const float fy = (ro.y - sc.grid_lo[1]) * sc.grid_inv[1];
+    const float fz = (ro.z - sc.grid_lo[2]) * sc.grid_inv[2];
+    constexpr float G = (float)GRID_G;
+    const float ax = __builtin_fabsf(rd.x), ay = __builtin_fabsf(rd.y), az = __builtin_fabsf(rd.z);
+    const bool kx = ax >= ay && ax >= az, ky = !kx && ay >= az;
+    const float m = kx ? ax : (ky ? ay : az);
+    const float dk = kx ? rd.x : (ky ? rd.y : rd.z);
+    const float di = kx ? rd.y : (ky ? rd.z : rd.x);     // axis k + 1
+    const float dj = kx ? rd.z : (ky ? rd.x : rd.y);     // axis k + 2
+    const bool ok = fx >= 0.f && fx < G && fy >= 0.f && fy < G && fz >= 0.f && fz < G &&   // false for NaN
+                    __builtin_isfinite(ax + ay + az) && m > 1e-30f;
+    const float r = __builtin_amdgcn_rcpf(m);
+    constexpr float HB = 0.5f * (float)GRID_B;
+    const int bu = __builtin_amdgcn_fmed3f(__builtin_truncf((di * r + 1.f) * HB), 0.f, (float)(GRID_B - 1));
+    const int bv = __builtin_amdgcn_fmed3f(__builtin_truncf((dj * r + 1.f) * HB), 0.f, (float)(GRID_B - 1));
+    const int face = (kx ? 0 : (ky ? 2 : 4)) + (dk > 0.f ? 1 : 0);
+    const int cell = ((int)fz * GRID_G + (int)fy) * GRID_G + (int)fx;
+    const int e = ok ? ((cell * 6 + face) * GRID_B + bu) * GRID_B + bv : 0;
+    const uint64_t sup = sc.grid[e];
+    return ok ? sup : sc.grid_all;
+}
 template <bool TIMING = false, bool NEAR_FIRST = false>
 PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeomHot* lgeoms, f3 ro, f3 rd, float& t_min, int& win,
                              f3& seed) {
@@ -862,14 +911,28 @@ PT_DEV void prim_intersect_q(const SceneDev& sc, const DevGeomHot* lgeoms, f3 ro
     if (NEAR_FIRST) {
         int first = -1;
         float best = __builtin_inff();
+        if (sc.grid) {   // camera rays of a wave share their cell and mostly their bin: a near-uniform loop
+            for (uint64_t m = grid_superset(sc, ro, rd); m != 0; m &= m - 1) {
+                const int i = __builtin_ctzll(m);
+                const float e = cull_entry(sc.geoms[i], cr);
+                if (e != __builtin_inff()) {
+                    cand |= 1ull << i;
+                    if (e < best) {
+                        best = e;
+                        first = i;
+                    }
+                }
+            }
+        } else {
 #pragma unroll 4
-        for (int i = 0; i < sc.num_geoms; ++i) {
-            const float e = cull_entry(sc.geoms[i], cr);
-            if (e != __builtin_inff()) {
-                cand |= 1ull << i;
-                if (e < best) {
-                    best = e;
-                    first = i;
+            for (int i = 0; i < sc.num_geoms; ++i) {
+                const float e = cull_entry(sc.geoms[i], cr);
+                if (e != __builtin_inff()) {
+                    cand |= 1ull << i;
+                    if (e < best) {
+                        best = e;
+                        first = i;
+                    }
                 }
             }
         }
@@ -1044,6 +1107,49 @@ PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3
         cand |= (uint64_t)bits << i0;
     }
     return cand;
+}
+
+PT_DEV uint64_t cull_candidates_grid(const SceneDev& sc, const float4* lc, const CullRay& cr, f3 ro, f3 rd,
+                                     bool bounded) {
+    uint64_t m = grid_superset(sc, ro, rd);
+    uint64_t cand = 0;
+    while (m != 0) {   // per lane: the wave runs as many rounds as its largest superset
+        const int i = __builtin_ctzll(m);
+        m &= m - 1;
+        const float4 A = lc[3 * i], B = lc[3 * i + 1], C = lc[3 * i + 2];
+        const float a0 = __builtin_fmaf(A.x, cr.id.x, -cr.rid.x), b0 = __builtin_fmaf(A.w, cr.id.x, -cr.rid.x);
+        const float a1 = __builtin_fmaf(A.y, cr.id.y, -cr.rid.y), b1 = __builtin_fmaf(B.x, cr.id.y, -cr.rid.y);
+        const float a2 = __builtin_fmaf(A.z, cr.id.z, -cr.rid.z), b2 = __builtin_fmaf(B.y, cr.id.z, -cr.rid.z);
+        const float t0 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(a0, b0), __builtin_fminf(a1, b1)),
+                                         __builtin_fmaxf(__builtin_fminf(a2, b2), -1e-2f));
+        const float t1 = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(a0, b0), __builtin_fmaxf(a1, b1)),
+                                         __builtin_fmaxf(a2, b2));
+        const uint32_t slab = (uint32_t)(t1 >= t0);
+        const uint32_t row = (uint32_t)(__float_as_int(C.z) != 0);
+        const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
+        const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
+        const uint32_t away = ((uint32_t)(qo > 0.5f) & (uint32_t)(u > 0.0f)) |
+                              ((uint32_t)(qo < -0.5f) & (uint32_t)(u < 0.0f));
+        const uint32_t keep = slab & ((away & (uint32_t)bounded & row) ^ 1u);
+        cand |= (uint64_t)keep << i;
+    }
+    return cand;
+}
+// float4s of the block's LDS geom table: the exact tests' DevGeomHot prefix of every geom, then
+// (candidate table on) the pre-test's DevCull records
+PT_DEV int lds_geom_f4(const SceneDev& sc) {
+    return sc.num_geoms * ((int)(sizeof(DevGeomHot) / 16) + (sc.grid ? 3 : 0));
+}
+PT_DEV void stage_geoms(const SceneDev& sc, float4* s_dyn) {
+    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
+    const float4* src = reinterpret_cast<const float4*>(sc.geoms);
+    const int nh = sc.num_geoms * HOT4;
+    for (int k = threadIdx.x; k < nh; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
+    if (sc.grid) {
+        const float4* cs = reinterpret_cast<const float4*>(sc.cull);
+        for (int k = threadIdx.x; k < 3 * sc.num_geoms; k += BLOCK) s_dyn[nh + k] = cs[k];
+    }
+    __syncthreads();
 }
 
 constexpr int WCAP = 192;      // pairs per wave held in LDS; more -> per-lane queue fallback
@@ -1251,6 +1357,7 @@ PT_DEV void group_by_material(int key, MatGroupLds* S, bool& active, bool& live,
     if (SPLIT) { qt = v[NW - 4]; qs = mk(v[NW - 3], v[NW - 2], v[NW - 1]); }
 }
 
+// lg: the block's LDS geom table (lds_geom_f4)
 template <bool TIMING = false>
 PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, f3 ro, f3 rd, BlockLds* B,
                             float& t_min, int& win, f3& seed) {
@@ -1262,7 +1369,9 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         cr = cull_ray(ro, rd);
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
-        cand = cull_candidates(sc, cr, ro, rd, bounded);
+        cand = sc.grid ? cull_candidates_grid(sc, reinterpret_cast<const float4*>(lg + sc.num_geoms), cr, ro, rd,
+                                              bounded)
+                       : cull_candidates(sc, cr, ro, rd, bounded);
         PT_HOOK(DUP_CULL, sc, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);

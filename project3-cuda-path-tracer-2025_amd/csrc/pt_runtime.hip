@@ -215,16 +215,11 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     uint64_t tc = TIMING ? sec_clock() : 0;
     const int tid = threadIdx.x;
     const bool lds_geoms = (QUEUE || REDIST) && sc.num_geoms <= LDS_GEOMS;
-    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
     DevGeomHot* s_geoms = reinterpret_cast<DevGeomHot*>(s_dyn);
-    int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? sc.num_geoms * HOT4 : 0));
+    int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? lds_geom_f4(sc) : 0));
     WaveLds* s_wave_isect =
         reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH && !SPLIT ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
-    if (lds_geoms) {   // per-lane candidate tests then read their geom from LDS, not L2
-        const float4* src = reinterpret_cast<const float4*>(sc.geoms);
-        for (int k = tid; k < sc.num_geoms * HOT4; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
-        __syncthreads();
-    }
+    if (lds_geoms) stage_geoms(sc, s_dyn);   // per-lane candidate tests then read their geom from LDS, not L2
     const int gid = block_start + tid;
     bool active = gid < n;
     PathReg p;
@@ -391,14 +386,9 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
     const int block_start = blockIdx.x * BLOCK;
     if (block_start >= n) return;
     const int tid = threadIdx.x, lane = tid & 63;
-    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
     DevGeomHot* s_geoms = reinterpret_cast<DevGeomHot*>(s_dyn);
-    BlockLds* s_block = reinterpret_cast<BlockLds*>(s_dyn + sc.num_geoms * HOT4);
-    {
-        const float4* src = reinterpret_cast<const float4*>(sc.geoms);
-        for (int k = tid; k < sc.num_geoms * HOT4; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
-        __syncthreads();
-    }
+    BlockLds* s_block = reinterpret_cast<BlockLds*>(s_dyn + lds_geom_f4(sc));
+    stage_geoms(sc, s_dyn);
     const int gid = block_start + tid;
     const bool active = gid < n;
     PathReg p;
@@ -917,6 +907,7 @@ struct State {
     float* d_image = nullptr;
     FrameCtl* d_ctl = nullptr;
     float* d_contrib = nullptr;      // passes of F > 1 frames: F planes of pixels_total float3
+    unsigned long long* d_grid = nullptr;   // the pre-test's candidate table (build_candidate_table)
     int batch = 1;                   // frames per pass (pt_options.frames_per_pass, resolved)
     bool split = false;              // VAR_BVH_SPLIT active (fused, fast BVH on the pair layout)
     bool no_tex = false;             // no textured / bump-mapped material (VAR_NO_TEX kernels)
@@ -998,6 +989,11 @@ void release_graph() {
     }
 }
 
+// bytes of the block's LDS geom table (lds_geom_f4 on the device)
+size_t geom_table_lds() {
+    return (sizeof(DevGeomHot) + (gp->sc.grid ? sizeof(DevCull) : 0)) * (size_t)gp->sc.num_geoms;
+}
+
 // device-side counter of the input of bounce b in the staged pipeline
 const int* staged_count(int b) { return &gp->d_ctl->cnt[b][0][0]; }
 
@@ -1005,7 +1001,7 @@ template <bool FIRST, bool HAS_BVH, int VAR>
 void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     constexpr bool SPLIT = HAS_BVH && (VAR & VAR_BVH_SPLIT);
     const bool lds = (VAR & (VAR_CAND_QUEUE | VAR_WAVE_REDIST)) && gp->sc.num_geoms <= LDS_GEOMS;
-    const size_t geom_lds = lds ? sizeof(DevGeomHot) * gp->sc.num_geoms : 0;
+    const size_t geom_lds = lds ? geom_table_lds() : 0;
     // the exchange's region: block_intersect's BlockLds, or one WaveLds per wave (wave_intersect)
     const size_t redist_lds = (VAR & VAR_WAVE_REDIST) && lds
                                   ? ((VAR & VAR_BLOCK_REDIST) ? sizeof(BlockLds) : sizeof(WaveLds) * (BLOCK / 64))
@@ -1156,7 +1152,7 @@ int enqueue_pass_body(int batch) {
         }
         if (t) {
             constexpr int V = VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST;
-            const size_t lds = sizeof(DevGeomHot) * gp->sc.num_geoms + sizeof(BlockLds);
+            const size_t lds = geom_table_lds() + sizeof(BlockLds);
             if (gp->no_tex)
                 launch(300 + t, k_tail<V | VAR_NO_TEX>, dim3(nb), dim3(BLOCK), lds, gp->sc, pathbuf(t & 1), gp->d_ctl,
                        gp->d_image, t, gp->seg_stride, depth);
@@ -1297,6 +1293,89 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
         if (nd.right >= 0) st.push_back({nd.right, d + 1});
     }
     return h;
+}
+
+// The pre-test's candidate table (SceneDev::grid, read by grid_superset): GRID_G^3 origin cells
+// over the scene x 6 dominant-axis faces x GRID_B^2 bins of the two other direction ratios
+// (d_i / |d_k| in [-1, 1]).  Entry bit g is set when SOME ray with its origin in the cell and its
+// direction in the bin can reach geom g's conservative world box at a nonnegative distance --
+// interval arithmetic in double along the dominant axis (the distance interval tau) and then on
+// the other two axes (origin interval + ratio interval x tau interval), a superset of the real
+// condition.  Every exact hit point lies in that box (the pre-test's premise, cull_geom), so a geom
+// outside the entry cannot be hit.  The cells are grown by far more than the device's float
+// cell computation can be off, the bins likewise for its rcp-based ratio, the boxes by 1e-6 of
+// the scene.  Returns false (no table) for scenes whose geom boxes are not finite.
+bool build_candidate_table(const std::vector<DevCull>& culls, int ng, const pt_vec3& cam,
+                           std::vector<unsigned long long>& table, float lo_out[3], float inv_out[3]) {
+    double lo[3] = {cam.x, cam.y, cam.z}, hi[3] = {cam.x, cam.y, cam.z};
+    for (int g = 0; g < ng; ++g)
+        for (int a = 0; a < 3; ++a) {
+            if (!(std::fabs(culls[g].lo[a]) < 1e17f && std::fabs(culls[g].hi[a]) < 1e17f)) return false;
+            lo[a] = std::min(lo[a], (double)culls[g].lo[a]);
+            hi[a] = std::max(hi[a], (double)culls[g].hi[a]);
+        }
+    double ext = 1.0;
+    for (int a = 0; a < 3; ++a) ext = std::max({ext, std::fabs(lo[a]), std::fabs(hi[a])});
+    double cs[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] -= 1e-3 * ext;
+        hi[a] += 1e-3 * ext;
+        lo_out[a] = (float)lo[a];
+        lo[a] = lo_out[a];                                  // the device's origin of the cells
+        inv_out[a] = (float)(GRID_G / (hi[a] - lo[a]));
+        cs[a] = 1.0 / (double)inv_out[a];                   // the device's cell size
+    }
+    const double cm = 1e-6 * ext, bin_eps = 1e-5;
+    const int G = GRID_G, B = GRID_B;
+    table.assign((size_t)G * G * G * 6 * B * B, 0ull);
+    std::vector<double> ta(ng), tb(ng);
+    std::vector<unsigned long long> mi(B), mj(B);
+    for (int cz = 0; cz < G; ++cz)
+        for (int cy = 0; cy < G; ++cy)
+            for (int cx = 0; cx < G; ++cx) {
+                const int c[3] = {cx, cy, cz};
+                double cl[3], ch[3];
+                for (int a = 0; a < 3; ++a) {
+                    cl[a] = lo[a] + c[a] * cs[a] - (1e-4 * cs[a] + cm);
+                    ch[a] = lo[a] + (c[a] + 1) * cs[a] + (1e-4 * cs[a] + cm);
+                }
+                const int cell = (cz * G + cy) * G + cx;
+                for (int face = 0; face < 6; ++face) {
+                    const int k = face / 2, i = (k + 1) % 3, j = (k + 2) % 3;
+                    const double s = (face & 1) ? 1.0 : -1.0;
+                    unsigned long long mk_ = 0;
+                    for (int g = 0; g < ng; ++g) {   // distance along axis k to reach the box's k-slab
+                        const double bl = culls[g].lo[k] - cm, bh = culls[g].hi[k] + cm;
+                        double a0 = s > 0 ? bl - ch[k] : cl[k] - bh, a1 = s > 0 ? bh - cl[k] : ch[k] - bl;
+                        a0 = std::max(a0, -cm);
+                        ta[g] = a0;
+                        tb[g] = a1;
+                        if (a1 >= a0) mk_ |= 1ull << g;
+                    }
+                    for (int axis = 0; axis < 2; ++axis) {
+                        const int a = axis == 0 ? i : j;
+                        std::vector<unsigned long long>& m = axis == 0 ? mi : mj;
+                        for (int b = 0; b < B; ++b) {
+                            const double r0 = (b == 0 ? -1.0 : -1.0 + 2.0 * b / B) - bin_eps;
+                            const double r1 = (b == B - 1 ? 1.0 : -1.0 + 2.0 * (b + 1) / B) + bin_eps;
+                            unsigned long long bits = 0;
+                            for (int g = 0; g < ng; ++g) {
+                                if (!((mk_ >> g) & 1)) continue;
+                                const double p[4] = {r0 * ta[g], r0 * tb[g], r1 * ta[g], r1 * tb[g]};
+                                const double pl = std::min({p[0], p[1], p[2], p[3]});
+                                const double ph = std::max({p[0], p[1], p[2], p[3]});
+                                if (cl[a] + pl <= (double)culls[g].hi[a] + cm && ch[a] + ph >= (double)culls[g].lo[a] - cm)
+                                    bits |= 1ull << g;
+                            }
+                            m[b] = bits;
+                        }
+                    }
+                    unsigned long long* row = &table[((size_t)cell * 6 + face) * B * B];
+                    for (int bu = 0; bu < B; ++bu)
+                        for (int bv = 0; bv < B; ++bv) row[bu * B + bv] = mi[bu] & mj[bv];
+                }
+            }
+    return true;
 }
 
 // Every inner node's box contains both children's boxes and every leaf's box contains its
@@ -1454,7 +1533,7 @@ void free_all() {
     release_graph();
     free_pass_buffers();
     void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_quads, gp->d_hot4,
-                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl};
+                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (gp->stream) (void)hipStreamDestroy(gp->stream);
@@ -2476,6 +2555,17 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     RC(dalloc(&gp->d_mats, mats.size()));
     RC(upload(gp->d_geoms, geoms.data(), geoms.size()));
     RC(dalloc(&gp->d_cull, culls.size()));
+    // the pre-test's candidate table, for scenes whose flat pre-test is long (PT_GRID=0: off, A/B)
+    std::vector<unsigned long long> grid;
+    float grid_lo[3] = {0.f, 0.f, 0.f}, grid_inv[3] = {0.f, 0.f, 0.f};
+    {
+        static const bool grid_off = getenv("PT_GRID") && atoi(getenv("PT_GRID")) == 0;
+        if (!grid_off && s->num_geoms >= GRID_MIN_GEOMS && s->num_geoms <= LDS_GEOMS &&
+            build_candidate_table(culls, s->num_geoms, s->camera.position, grid, grid_lo, grid_inv)) {
+            RC(dalloc(&gp->d_grid, grid.size()));
+            RC(upload(gp->d_grid, grid.data(), grid.size()));
+        }
+    }
     RC(upload(gp->d_cull, culls.data(), culls.size()));
     RC(upload(gp->d_mats, mats.data(), mats.size()));
     if (gp->has_bvh) {
@@ -2570,6 +2660,12 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     // bounds from s = sx on the device, rounded up
     sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
     sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
+    sc.grid = gp->d_grid;
+    sc.grid_all = s->num_geoms >= 64 ? ~0ull : ((1ull << s->num_geoms) - 1);
+    for (int a = 0; a < 3; ++a) {
+        sc.grid_lo[a] = grid_lo[a];
+        sc.grid_inv[a] = grid_inv[a];
+    }
     RC(ensure_frames(1));            // one frame's wavefront now; larger passes grow it on first use
     gp->inited = true;
     HIPCHK(hipDeviceSynchronize());

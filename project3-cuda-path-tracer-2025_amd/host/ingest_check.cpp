@@ -1,0 +1,107 @@
+// ingest_check.cpp — the host ingest behind the C-ABI, driven standalone for the sanitizer build
+// (Makefile target `asan`: host/*.cpp with -fsanitize=address,undefined, no device code).
+//
+// The files a caller hands the library are untrusted: scene JSON (host/json_lite.h), OBJ meshes
+// (host/scene.cpp's reader) and PNG textures (host/png_decode.cpp, a from-scratch inflate).  The
+// reference's failure semantics are an exception for a scene it cannot read (scene.cpp:245-247,
+// "Failed to load") and -1 for a texture it cannot decode (scene.cpp:372-375, shown as magenta);
+// here: PT_E_INVALID with a message, and textureID -1.  Every input must end in one of those or
+// in a loaded scene -- never in a sanitizer report.
+//
+//   ingest_check scene FILE.json...   pt_scene_load_ex (host BVH) + the SAH traversal tree over its
+//                                     leaves + pt_scene_get_view; prints "scene rc=<rc> ..."
+//   ingest_check png FILE...          pt_texture_load (size query, then decode); "png rc=<rc> w h"
+//   ingest_check savepng OUT W H      pt_save_png of a W x H test image with NaN / inf / negatives
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "pt/pathtrace_abi.h"
+#include "trav_tree.h"
+
+static int check_scene(const char* path) {
+    pt_scene_file* f = nullptr;
+    const int rc = pt_scene_load_ex(path, -1, -1, -1, PT_SCENE_VIEWER_CAMERA, &f);
+    if (rc != PT_OK) {
+        std::printf("scene rc=%d err=%s\n", rc, pt_scene_last_error());
+        return rc;
+    }
+    pt_scene_view v{};
+    pt_scene_get_view(f, &v);
+    int32_t iters = 0, depth = 0;
+    char name[256];
+    pt_scene_get_info(f, &iters, &depth, name, (int32_t)sizeof name);
+    int bad_tex = 0;
+    for (int i = 0; i < v.num_materials; ++i) {
+        char mname[128];
+        pt_scene_material_name(f, i, mname, (int32_t)sizeof mname);
+        if ((v.materials[i].hasTexture && v.materials[i].textureID < 0) ||
+            (v.materials[i].hasBumpMap && v.materials[i].bumpID < 0))
+            ++bad_tex;
+    }
+    // the SAH traversal hierarchy pt_init builds over the BVH's leaves (host part of the path)
+    std::vector<float> lo, hi, s;
+    for (int i = 0; i < v.num_bvh_nodes; ++i) {
+        const pt_bvh_node& nd = v.bvh_nodes[i];
+        if (!(nd.triCount > 0 && nd.start >= 0)) continue;
+        const float l[3] = {nd.aabb.min.x, nd.aabb.min.y, nd.aabb.min.z};
+        const float h[3] = {nd.aabb.max.x, nd.aabb.max.y, nd.aabb.max.z};
+        for (int a = 0; a < 3; ++a) {
+            lo.push_back(l[a]);
+            hi.push_back(h[a]);
+        }
+        s.push_back(1.0f);
+    }
+    std::vector<pth::TravInner> tree;
+    int height = 0;
+    const bool sah = pth::build_sah_tree(lo, hi, s, tree, height);
+    std::printf("scene rc=0 geoms=%d materials=%d triangles=%d nodes=%d depth=%d textures=%d bad_tex=%d sah=%d\n",
+                v.num_geoms, v.num_materials, v.num_triangles, v.num_bvh_nodes, depth, v.num_textures, bad_tex,
+                sah ? height : -1);
+    pt_scene_free(f);
+    return 0;
+}
+
+static int check_png(const char* path) {
+    int32_t w = 0, h = 0;
+    int rc = pt_texture_load(path, &w, &h, nullptr, 0);
+    if (rc == PT_OK) {
+        std::vector<uint8_t> px((size_t)w * h * 4);
+        rc = pt_texture_load(path, &w, &h, px.data(), (int64_t)px.size());
+    }
+    if (rc != PT_OK) std::printf("png rc=%d err=%s\n", rc, pt_scene_last_error());
+    else std::printf("png rc=0 %d %d\n", w, h);
+    return rc;
+}
+
+static int save_png(const char* out, int w, int h) {
+    std::vector<float> img((size_t)w * h * 3);
+    for (size_t i = 0; i < img.size(); ++i) img[i] = (float)((i * 37) % 300) / 7.0f - 3.0f;
+    if (!img.empty()) img[0] = std::numeric_limits<float>::quiet_NaN();
+    if (img.size() > 1) img[1] = std::numeric_limits<float>::infinity();
+    if (img.size() > 2) img[2] = -std::numeric_limits<float>::infinity();
+    const int rc = pt_save_png(img.data(), w, h, 3, out);
+    std::printf("savepng rc=%d\n", rc);
+    return rc;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        std::fprintf(stderr, "usage: %s scene|png FILE... | savepng OUT W H\n", argv[0]);
+        return 2;
+    }
+    const std::string mode = argv[1];
+    if (mode == "savepng" && argc == 5) return save_png(argv[2], std::atoi(argv[3]), std::atoi(argv[4])) == 0 ? 0 : 1;
+    for (int i = 2; i < argc; ++i) {
+        std::printf("%s: ", argv[i]);
+        if (mode == "scene") check_scene(argv[i]);
+        else if (mode == "png") check_png(argv[i]);
+        else return 2;
+        std::fflush(stdout);
+    }
+    return 0;
+}

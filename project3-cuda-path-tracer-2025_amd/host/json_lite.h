@@ -43,8 +43,20 @@ struct Value {
     }
     int as_int() const {
         if (kind == Int) return static_cast<int>(i);
-        if (kind == Float) return static_cast<int>(f);
+        // static_cast like get<int>(); a value outside int (or NaN) has no defined conversion
+        if (kind == Float && f > -2147483649.0 && f < 2147483648.0) return static_cast<int>(f);
+        if (kind == Float) throw std::runtime_error("json: number out of int range");
         throw std::runtime_error("json: not a number");
+    }
+    // iteration as nlohmann presents it to scene.cpp: `for (auto& p : objectsData)` over a non-array
+    // and `item.key()` over a non-object throw type_error there
+    const std::vector<Value>& as_array() const {
+        if (kind != Array) throw std::runtime_error("json: not an array");
+        return arr;
+    }
+    const std::map<std::string, Value>& as_object() const {
+        if (kind != Object) throw std::runtime_error("json: not an object");
+        return obj;
     }
     const std::string& as_string() const {
         if (kind != String) throw std::runtime_error("json: not a string");
@@ -65,6 +77,8 @@ public:
 private:
     const std::string& t_;
     size_t p_ = 0;
+    int depth_ = 0;   // nesting of arrays / objects (recursive descent: bounded, not the C++ stack)
+    static constexpr int kMaxDepth = 256;
 
     [[noreturn]] void err(const char* m) { throw std::runtime_error(std::string("json: ") + m + " at offset " + std::to_string(p_)); }
     void ws() {
@@ -77,8 +91,12 @@ private:
     }
     Value value() {
         char c = peek();
-        if (c == '{') return object();
-        if (c == '[') return array();
+        if (c == '{' || c == '[') {
+            if (++depth_ > kMaxDepth) err("nesting too deep");
+            Value v = c == '{' ? object() : array();
+            --depth_;
+            return v;
+        }
         if (c == '"') { Value v; v.kind = Value::String; v.s = str(); return v; }
         if (c == 't' || c == 'f' || c == 'n') return literal();
         return number();

@@ -84,8 +84,10 @@ const uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97,
 const uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6,
                                 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 
-bool inflate_codes(BitReader& br, const Huffman& lit, const Huffman& dist, std::vector<uint8_t>& out, std::string& err) {
+bool inflate_codes(BitReader& br, const Huffman& lit, const Huffman& dist, std::vector<uint8_t>& out, size_t max_out,
+                   std::string& err) {
     for (;;) {
+        if (out.size() > max_out) return err = "inflate: more data than the image holds", false;
         int sym = lit.decode(br);
         if (sym < 0) return err = "inflate: bad literal/length code", false;
         if (sym < 256) {
@@ -107,7 +109,7 @@ bool inflate_codes(BitReader& br, const Huffman& lit, const Huffman& dist, std::
     }
 }
 
-bool inflate_raw(const uint8_t* data, size_t size, std::vector<uint8_t>& out, std::string& err) {
+bool inflate_raw(const uint8_t* data, size_t size, std::vector<uint8_t>& out, size_t max_out, std::string& err) {
     BitReader br{data, size};
     int last = 0;
     do {
@@ -121,6 +123,7 @@ bool inflate_raw(const uint8_t* data, size_t size, std::vector<uint8_t>& out, st
             br.pos += 4;
             if ((len ^ 0xffffu) != nlen) return err = "inflate: stored length mismatch", false;
             if (br.pos + len > size) return err = "inflate: truncated stored block", false;
+            if (out.size() + len > max_out) return err = "inflate: more data than the image holds", false;
             out.insert(out.end(), data + br.pos, data + br.pos + len);
             br.pos += len;
         } else if (type == 1) {                            // fixed Huffman
@@ -133,7 +136,7 @@ bool inflate_raw(const uint8_t* data, size_t size, std::vector<uint8_t>& out, st
             Huffman lit, dist;
             lit.build(l, 288);
             dist.build(d, 30);
-            if (!inflate_codes(br, lit, dist, out, err)) return false;
+            if (!inflate_codes(br, lit, dist, out, max_out, err)) return false;
         } else if (type == 2) {                            // dynamic Huffman
             int hlit = (int)br.bits(5) + 257, hdist = (int)br.bits(5) + 1, hclen = (int)br.bits(4) + 4;
             static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -167,7 +170,7 @@ bool inflate_raw(const uint8_t* data, size_t size, std::vector<uint8_t>& out, st
             Huffman lit, dist;
             if (!lit.build(lens, hlit) || !dist.build(lens + hlit, hdist))
                 return err = "inflate: bad literal/distance code", false;
-            if (!inflate_codes(br, lit, dist, out, err)) return false;
+            if (!inflate_codes(br, lit, dist, out, max_out, err)) return false;
         } else {
             return err = "inflate: reserved block type", false;
         }
@@ -212,12 +215,12 @@ bool unfilter(uint8_t* img, size_t rows, size_t stride, size_t bpp, std::vector<
 
 }  // namespace
 
-bool zlib_inflate(const uint8_t* data, size_t size, std::vector<uint8_t>& out, std::string& err) {
+bool zlib_inflate(const uint8_t* data, size_t size, std::vector<uint8_t>& out, std::string& err, size_t max_out) {
     if (size < 2) return err = "zlib: stream too short", false;
     const int cmf = data[0], flg = data[1];
     if ((cmf & 15) != 8 || ((cmf << 8) | flg) % 31 != 0) return err = "zlib: bad header", false;
     if (flg & 32) return err = "zlib: preset dictionary not supported", false;
-    return inflate_raw(data + 2, size - 2, out, err);
+    return inflate_raw(data + 2, size - 2, out, max_out, err);
 }
 
 bool png_decode_rgba(const uint8_t* data, size_t size, int& w, int& h, std::vector<uint8_t>& rgba, std::string& err) {
@@ -271,11 +274,25 @@ bool png_decode_rgba(const uint8_t* data, size_t size, int& w, int& h, std::vect
     if (ctype == 3 && plte.empty()) return err = "png: palette image without PLTE", false;
     if (interlace > 1) return err = "png: bad interlace method", false;
 
-    std::vector<uint8_t> raw;
-    if (!zlib_inflate(idat.data(), idat.size(), raw, err)) return false;
-
     const size_t bits_pp = (size_t)chans * depth;
     const size_t bpp = (bits_pp + 7) / 8;                  // filter unit
+    // the filtered data the header promises: checked before anything image-sized is allocated, and
+    // the inflate stops there (a small file cannot make it allocate more than the image holds)
+    size_t need = 0;
+    if (interlace == 0) {
+        need = (size_t)H * (((size_t)W * bits_pp + 7) / 8 + 1);
+    } else {
+        static const int xo[7] = {0, 4, 0, 2, 0, 1, 0}, yo[7] = {0, 0, 4, 0, 2, 0, 1};
+        static const int xs[7] = {8, 8, 4, 4, 2, 2, 1}, ys[7] = {8, 8, 8, 4, 4, 2, 2};
+        for (int p = 0; p < 7; ++p) {
+            const size_t sw = W > (uint32_t)xo[p] ? (W - xo[p] + xs[p] - 1) / xs[p] : 0;
+            const size_t sh = H > (uint32_t)yo[p] ? (H - yo[p] + ys[p] - 1) / ys[p] : 0;
+            if (sw && sh) need += sh * ((sw * bits_pp + 7) / 8 + 1);
+        }
+    }
+    std::vector<uint8_t> raw;
+    if (!zlib_inflate(idat.data(), idat.size(), raw, err, need + 65536)) return false;
+    if (raw.size() < need) return err = "png: image data shorter than the header says", false;
     // decoded samples at native depth, one row of W pixels per image row
     std::vector<uint16_t> samp((size_t)W * H * chans);
     auto read_rows = [&](const uint8_t* src, size_t sw, size_t sh, int x0, int y0, int dx, int dy,
@@ -286,7 +303,7 @@ bool png_decode_rgba(const uint8_t* data, size_t size, int& w, int& h, std::vect
         }
         const size_t stride = (sw * bits_pp + 7) / 8;
         consumed = sh * (stride + 1);
-        if (src + consumed > raw.data() + raw.size()) return false;
+        if ((size_t)(src - raw.data()) + consumed > raw.size()) return false;
         std::vector<uint8_t> tmp(src, src + consumed), rows;
         if (!unfilter(tmp.data(), sh, stride, bpp, rows)) return false;
         for (size_t y = 0; y < sh; ++y) {

@@ -17,7 +17,8 @@ namespace ptio {
 bool png_load_rgba(const std::string& path, int& w, int& h, std::vector<uint8_t>& rgba, std::string& err);
 bool png_decode_rgba(const uint8_t* data, size_t size, int& w, int& h, std::vector<uint8_t>& rgba, std::string& err);
 
-// raw zlib stream -> bytes (exposed for tests)
-bool zlib_inflate(const uint8_t* data, size_t size, std::vector<uint8_t>& out, std::string& err);
+// raw zlib stream -> bytes (exposed for tests); fails once the output would exceed max_out
+bool zlib_inflate(const uint8_t* data, size_t size, std::vector<uint8_t>& out, std::string& err,
+                  size_t max_out = (size_t)1 << 31);
 
 }  // namespace ptio

@@ -209,6 +209,8 @@ void parse_obj(const std::string& path, std::vector<float>& pos, std::vector<flo
                                         resolve(parts[2], nrm.size() / 3)});
             }
             if (poly.size() < 3) continue;
+            for (const ObjIndex& ix : poly)   // before the quad split reads positions
+                if (ix.v < 0 || 3 * (size_t)ix.v + 2 >= pos.size()) throw std::runtime_error("bad vertex index in " + path);
             if (poly.size() == 3) {
                 faces.insert(faces.end(), poly.begin(), poly.end());
             } else if (poly.size() == 4) {
@@ -383,7 +385,7 @@ void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int de
     ptj::Value data = ptj::parse(read_file(jsonName));
     const ptj::Value& materialsData = data["Materials"];
     std::map<std::string, int> MatNameToID;
-    for (const auto& item : materialsData.obj) {   // std::map order == nlohmann object order
+    for (const auto& item : materialsData.as_object()) {   // std::map order == nlohmann object order
         const std::string& name = item.first;
         const ptj::Value& p = item.second;
         Material m{};
@@ -444,7 +446,7 @@ void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int de
         auto it = MatNameToID.find(p["MATERIAL"].as_string());
         return it == MatNameToID.end() ? 0 : it->second;
     };
-    for (const ptj::Value& p : data["Objects"].arr) {
+    for (const ptj::Value& p : data["Objects"].as_array()) {
         const std::string& type = p["TYPE"].as_string();
         if (type == "obj") {
             size_t lastSlashPos = jsonName.find_last_of("/\\");
@@ -472,6 +474,11 @@ void Scene::loadFromJSON(const std::string& jsonName, int resx, int resy, int de
     camera = Camera{};
     camera.resolution.x = resx > 0 ? resx : cd["RES"][0].as_int();
     camera.resolution.y = resy > 0 ? resy : cd["RES"][1].as_int();
+    // the wavefront indexes pixels with 32-bit ints (the reference's too): a frame of at most 2^28
+    if (camera.resolution.x <= 0 || camera.resolution.y <= 0 || camera.resolution.x > 65536 ||
+        camera.resolution.y > 65536 || (int64_t)camera.resolution.x * camera.resolution.y > (int64_t(1) << 28))
+        throw std::runtime_error("bad RES " + std::to_string(camera.resolution.x) + "x" +
+                                 std::to_string(camera.resolution.y));
     float fovy = cd["FOVY"].as_float();
     state.iterations = (unsigned)cd["ITERATIONS"].as_int();
     state.traceDepth = depth >= 0 ? depth : cd["DEPTH"].as_int();
@@ -542,6 +549,9 @@ void Scene::buildBVH() {
     for (int i = 0; i < (int)triangles.size(); i++) triIndices[i] = i;
     if (triangles.empty()) return;
     if (gpuBVH) {   // the same recursion on the GPU (csrc/pt_bvh_build.hip), same bits
+#ifdef PT_HOST_ONLY   // the sanitizer build of the ingest (Makefile `asan`): no device code linked
+        throw std::runtime_error("GPU BVH build: not in this host-only build");
+#else
         const int n = (int)triangles.size();
         bvhNodes.resize(2 * (size_t)n - 1);
         int32_t count = 0;
@@ -550,6 +560,7 @@ void Scene::buildBVH() {
         if (rc != PT_OK) throw std::runtime_error(std::string("GPU BVH build: ") + pt_bvh_build_last_error());
         bvhNodes.resize((size_t)count);
         return;
+#endif
     }
     bvhNodes.reserve(2 * triangles.size());
     BVHBuilder b{triangles, bvhNodes, triIndices};

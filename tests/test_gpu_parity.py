@@ -368,6 +368,37 @@ def test_more_geoms_than_lds_table(opts, tmp_path, oracle, ptamd):
     tr.free()
 
 
+@pytest.mark.parametrize("n,res,iters", [(12, (64, 64), 3), (33, (64, 64), 3), (55, (48, 48), 2)])
+def test_candidate_table_scenes_bitexact(n, res, iters, tmp_path, oracle, ptamd):
+    """Scenes of GRID_MIN_GEOMS..64 geoms run the pre-test from the candidate table (a per-lane
+    superset of the geoms a ray from its origin cell in its direction bin can hit): random cubes
+    and spheres, rotated and scaled, mirrors and glass sending rays everywhere, two objects
+    outside the room (origins outside the walls) -- bit-exact against the oracle, live counts too."""
+    path = _many_geoms_scene(tmp_path / "grid.json", n)
+    with open(path) as f:
+        d = json.load(f)
+    d["Objects"] += [{"TYPE": "sphere", "MATERIAL": "mirror", "TRANS": [0, 5, 14], "ROTAT": [0, 0, 0],
+                      "SCALE": [3, 3, 3]},
+                     {"TYPE": "cube", "MATERIAL": "diffuse_white", "TRANS": [-9, 2, 0], "ROTAT": [10, 20, 30],
+                      "SCALE": [1, 6, 2]}]
+    with open(path, "w") as f:
+        json.dump(d, f)
+    a, b = _oracle_pair(oracle, ptamd, path, res)
+    assert 16 <= len(b.geoms) <= 64
+    tr = ptamd.PathTracer(b)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    for it in range(1, iters + 1):
+        live = r.trace(it)
+        tr.trace(it)
+        assert tr.stats()["live"] == [int(x) if x >= 0 else 0 for x in live]
+    assert _eq(tr.image(), r.image)
+    tr.trace_frames(iters + 1, 4)
+    for it in range(iters + 1, iters + 5):
+        r.trace(it)
+    assert _eq(tr.image(), r.image)
+    tr.free()
+
+
 def test_prepared_graphs_equal_oracle(oracle, ptamd):
     """pt_prepare_frames captures the pass graphs a later pt_trace_frames replays (bench.py keeps
     the capture out of its timed region); the frames traced through them equal the oracle."""
