@@ -44,10 +44,12 @@ using namespace ptd;
 
 // Fold the previous pass's live counts into the running totals, advance (or set) the
 // iteration, zero the per-pass counters and start a pass of `batch` frames.  One block.
-__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int batch) {
+// `rows`: the counter rows any pass since the last reset of the block wrote (trace depth + 1 at
+// most; the rest stay zero), so a frame clears 9 rows of 8 segments at depth 8, not 65.
+__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int batch, int rows) {
     int t = threadIdx.x;
     if (ctl->frames > 0) {
-        for (int b = t; b < MAXB + 1; b += blockDim.x) {
+        for (int b = t; b < rows; b += blockDim.x) {
             unsigned long long s = 0;
             for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k][0];
             ctl->tot[b] += s;
@@ -55,8 +57,8 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
         }
     }
     __syncthreads();
-    for (int i = t; i < (MAXB + 1) * NSEG * CNT_PAD; i += blockDim.x) (&ctl->cnt[0][0][0])[i] = 0;
-    for (int i = t; i < (MAXB + 1) * CNT_PAD; i += blockDim.x) (&ctl->qcnt[0][0])[i] = 0;
+    for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->cnt[0][0][0])[i * CNT_PAD] = 0;
+    for (int i = t; i < rows; i += blockDim.x) ctl->qcnt[i][0] = 0;
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
@@ -916,6 +918,8 @@ struct State {
     hipGraph_t graph[MAXF + 1] = {};
     hipGraphExec_t graph_exec[MAXF + 1] = {};
     int last_iter = 0;
+    int dev_iter = 0;                // FrameCtl::iter after the passes queued so far (0 after a reset)
+    int ctl_rows = 1;                // counter rows k_frame_begin folds / clears (max trace depth + 1)
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
     int key_bits = 1;
@@ -938,6 +942,14 @@ hipError_t smemcpy(void* dst, const void* src, size_t n, hipMemcpyKind kind) {
 }
 
 PathBuf pathbuf(int i) { return PathBuf{gp->d_path[i][0], gp->d_path[i][1], gp->d_path[i][2]}; }
+
+// zero the frame control block (counters, totals, the device iteration)
+int ctl_reset() {
+    const hipError_t e = smemset(gp->d_ctl, 0, sizeof(FrameCtl));
+    if (e != hipSuccess) return fail(PT_E_HIP, "FrameCtl reset: %s", hipGetErrorString(e));
+    gp->dev_iter = 0;
+    return PT_OK;
+}
 
 // pt_profile_frames: every kernel of the frame is launched with hipExtLaunchKernel's start/stop
 // events, which take their timestamps from that dispatch packet itself -- the kernel's own
@@ -1205,7 +1217,8 @@ int enqueue_pass_body(int batch) {
 }
 
 int enqueue_pass(int set_iter, int batch) {
-    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, gp->d_ctl, set_iter, gp->local_pixels, batch);
+    gp->ctl_rows = std::max(gp->ctl_rows, std::min(MAXB + 1, gp->sc.trace_depth + 1));
+    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, gp->d_ctl, set_iter, gp->local_pixels, batch, gp->ctl_rows);
     HIPCHK(hipGetLastError());
     RC(enqueue_pass_body(batch));
     if (batch > 1) {
@@ -1231,14 +1244,21 @@ int build_graph(int batch) {
 // one pass: frames iter .. iter + batch - 1
 int run_pass(int iter, int batch) {
     RC(ensure_frames(batch));
-    if (gp->opts.use_graph) {
+    // a single-frame pass (the API's pathtrace(), one call per frame) is launched directly: its six
+    // kernels run back to back either way, and a graph launch costs the host ~10 us more before
+    // its first kernel starts (tools/api_trace.py; PT_F1_GRAPH=1 keeps the graph, A/B)
+    static const bool f1_graph = getenv("PT_F1_GRAPH") && atoi(getenv("PT_F1_GRAPH")) != 0;
+    if (gp->opts.use_graph && (batch > 1 || f1_graph)) {
         if (!gp->graph_exec[batch]) RC(build_graph(batch));
-        // the graph's k_frame_begin increments: preset iter - 1 (stream-ordered)
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&gp->d_ctl->iter, iter - 1, 1, gp->stream));
+        // the graph's k_frame_begin advances the device iteration by one: preset iter - 1 (stream-
+        // ordered) unless the last pass left it there -- main.cpp's pathtrace(pbo, 0, ++iteration)
+        // calls then launch the graph alone
+        if (gp->dev_iter != iter - 1) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&gp->d_ctl->iter, iter - 1, 1, gp->stream));
         HIPCHK(hipGraphLaunch(gp->graph_exec[batch], gp->stream));
     } else {
         RC(enqueue_pass(iter, batch));
     }
+    gp->dev_iter = iter;
     gp->last_iter = iter + batch - 1;
     gp->frames_done += batch;
     return PT_OK;
@@ -2615,7 +2635,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     RC(dalloc(&gp->d_image, (size_t)gp->pixels_total * 3));
     HIPCHK(smemset(gp->d_image, 0, sizeof(float) * 3 * (size_t)gp->pixels_total));
     RC(dalloc(&gp->d_ctl, 1));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     gp->key_bits = 1;
     while ((1 << gp->key_bits) < std::max(2, s->num_materials)) gp->key_bits++;
 
@@ -2944,7 +2964,7 @@ int32_t pt_reset_stats(void) {
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         HIPCHK(hipStreamSynchronize(gp->stream));
-        HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+        RC(ctl_reset());
     }
     return PT_OK;
 }
@@ -2957,14 +2977,15 @@ int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(need_single("pt_test_camera"));
     if (!out || n < gp->local_pixels) return fail(PT_E_INVALID, "output too small");
     RC(ensure_frames(1));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
-    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, gp->stream, gp->d_ctl, iteration, gp->local_pixels, 1);
+    RC(ctl_reset());
+    hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, gp->stream, gp->d_ctl, iteration, gp->local_pixels, 1,
+                       gp->ctl_rows);
     hipLaunchKernelGGL(k_camera, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->stream, gp->sc, pathbuf(0), gp->d_ctl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(gp->stream));
     release_graph();
     RC(download_paths(0, gp->local_pixels, out));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     return PT_OK;
 }
 
@@ -3027,7 +3048,7 @@ int32_t pt_test_intersect(const pt_path_segment* paths, int64_t n, pt_shadeable_
         }
     }
     release_graph();
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     return PT_OK;
 }
 
@@ -3067,7 +3088,7 @@ int32_t pt_test_shade(int32_t iteration, const pt_shadeable_isect* isects, pt_pa
     HIPCHK(hipStreamSynchronize(gp->stream));
     release_graph();
     RC(download_paths(0, n, paths));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     return PT_OK;
 }
 
@@ -3079,7 +3100,7 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     std::vector<int> al(std::max<int64_t>(1, n));
     for (int64_t i = 0; i < n; ++i) al[i] = paths[i].remainingBounces > 0;   // PathAlive
     if (n) HIPCHK(smemcpy(gp->d_alive, al.data(), n * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     RC(set_count(0, (int)n));
     if (n > 0) {   // the pipeline's launch sequence
         launch_compact<CITEMS>(pathbuf(0), pathbuf(1), staged_count(0), &gp->d_ctl->cnt[1][0][0], (int)n);
@@ -3091,7 +3112,7 @@ int32_t pt_test_compact(const pt_path_segment* paths, int64_t n, pt_path_segment
     if (alive_out) *alive_out = na;
     release_graph();
     RC(download_paths(1, na, out));
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     return PT_OK;
 }
 
@@ -3118,7 +3139,7 @@ int32_t pt_test_sort(const pt_shadeable_isect* isects, int64_t n, int32_t* perm)
     HIPCHK(hipStreamSynchronize(gp->stream));
     HIPCHK(smemcpy(perm, gp->d_perm, n * sizeof(int), hipMemcpyDeviceToHost));
     release_graph();
-    HIPCHK(smemset(gp->d_ctl, 0, sizeof(FrameCtl)));
+    RC(ctl_reset());
     return PT_OK;
 }
 
@@ -3203,6 +3224,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
         const int f = pass_frames(count - i);
         pass_start.push_back(rec.size());
         rc = enqueue_pass(first_iteration + i, f);
+        gp->dev_iter = first_iteration + i;
         gp->frames_done += f;
         gp->last_iter = first_iteration + i + f - 1;
         i += f;
