@@ -32,8 +32,8 @@ enum : int {
                            // queued and traversed (then shaded) by k_bvh_bounce in full waves
     VAR_BVH_NODES = 64,    // host only: BVH_FAST on the node array instead of the DevPair layout (A/B)
     VAR_BLOCK_REDIST = 128,  // with VAR_WAVE_REDIST: the exchange spans the block (block_intersect)
-    VAR_BVH_QUAD = 256,    // with VAR_BVH_FAST + pair layout: traverse 4-wide nodes (DevQuad) collapsed
-                           // from the binary tree (same leaves, same winner)
+    VAR_BVH_Q32 = 256,     // host-set (k_bvh_bounce): the pair layout in 32-B quantized records (DevPairQ)
+                           // for scenes where the node fetches, not the decoding, bind the traversal
     VAR_MAT_GROUP = 512,   // fused MATERIAL_SORTING: the block's paths regrouped by material between
                            // intersection and shading (group_by_material); set by pt_options.material_sort
     VAR_NO_TEX = 1024,     // host-set: no material samples a texture or bump map, so the fused kernels'
@@ -76,8 +76,8 @@ struct SceneDev {
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
-    const DevQuad* quads;     // VAR_BVH_QUAD layout (null: not built); leaves are refs >= num_quads
-    int num_quads, qroot_ref;
+    const DevPairQ* pairq;    // VAR_BVH_Q32 layout (null: not built), same refs as `pairs`
+    const float4* leafbox;    // per leaf: its exact reference box (lo.xyz | -, hi.xyz | -)
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
@@ -579,114 +579,128 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
     return st.t_hit;
 }
 
-// one step on the 4-wide layout: a quad expansion (4 exact box decisions + certified culls, the
-// nearest passing child continues, the others are pushed farthest first) or one leaf
+// VAR_BVH_Q32: expand st.cur from its 32-B quantized record (DevPairQ).  The decoded boxes contain
+// the children's boxes; the decisions are aabb_fast / aabb_decide's on them (a containing box
+// passes whenever the contained one does), the culls cull_threshold's certified bound for the
+// shared class size.  A leaf child is entered on its decoded box and decided on its own exact
+// box by trav_leaf_q.
+PT_DEV float cull_class_size(uint32_t c) {
+    // 2^(k/4) for k = 0..3, each rounded up to float: s_q >= 2^((c - 128) / 4)
+    const float f = (c & 3) == 0 ? 1.0f : (c & 3) == 1 ? 1.18920720f : (c & 3) == 2 ? 1.41421366f : 1.68179286f;
+    return __builtin_ldexpf(f, (int)(c >> 2) - 32);
+}
 template <bool COUNT = false>
-PT_DEV void trav_step_quad(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
-    const int Q = sc.num_quads;
+PT_DEV bool trav_inner_q(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
     const float t_best = st.t_hit;
-    const int cur = st.cur;
-    bool next = false;
-    if (cur < Q) {
-        if (COUNT) n_nodes++;
-        const v4f* R = reinterpret_cast<const v4f*>(sc.quads + cur);
-        v4f lo[4], hi[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            lo[k] = R[k];
-            hi[k] = R[4 + k];
-        }
-        float e[4], T[4];
-        int r[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            r[k] = __float_as_int(lo[k][3]);
-            float ek = 0.f;
-            bool pk = r[k] >= 0 && aabb_decide(make_float4(lo[k][0], lo[k][1], lo[k][2], 0.f),
-                                               make_float4(hi[k][0], hi[k][1], hi[k][2], 0.f), st.ro, st.rd, st.rr,
-                                               st.exact, ek);
-            T[k] = pk ? cull_threshold(sc, ek, hi[k][3]) : 0.f;
-            pk = pk && !(t_best < T[k]);
-            e[k] = pk ? ek : __builtin_inff();
-            r[k] = pk ? r[k] : -1;
-        }
-        // nearest first: sort the 4 (entry, ref, T) by entry (5 compare-exchanges)
-        auto cx = [&](int a, int b) {
-            const bool sw = e[b] < e[a];
-            const float ea = e[a], ta = T[a];
-            const int ra = r[a];
-            e[a] = sw ? e[b] : ea; e[b] = sw ? ea : e[b];
-            T[a] = sw ? T[b] : ta; T[b] = sw ? ta : T[b];
-            r[a] = sw ? r[b] : ra; r[b] = sw ? ra : r[b];
-        };
-        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-        // refs of passing children in ascending entry order (NaN-free keys; -1 = none)
-        int first = -1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (first < 0 && r[k] >= 0) first = k;
-        if (first >= 0) {
-#pragma unroll
-            for (int k = 3; k >= 0; --k)
-                if (k != first && r[k] >= 0 && st.sp < sc.stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(r[k], T[k]);
-            st.cur = first == 0 ? r[0] : first == 1 ? r[1] : first == 2 ? r[2] : r[3];
-            next = true;
+    if (COUNT) n_nodes++;
+    const v4f* R = reinterpret_cast<const v4f*>(sc.pairq + st.cur);
+    const v4f w0 = R[0], w1 = R[1];
+    const uint32_t meta = __float_as_uint(w0[3]);
+    const float sx = __builtin_ldexpf(1.0f, (int)(meta & 255u) - 128);
+    const float sy = __builtin_ldexpf(1.0f, (int)((meta >> 8) & 255u) - 128);
+    const float sz = __builtin_ldexpf(1.0f, (int)((meta >> 16) & 255u) - 128);
+    const uint32_t q0 = __float_as_uint(w1[0]), q1 = __float_as_uint(w1[1]), q2 = __float_as_uint(w1[2]);
+    auto B = [](uint32_t w, int k) { return (float)((w >> (8 * k)) & 255u); };
+    const float4 l_lo = make_float4(__builtin_fmaf(B(q0, 0), sx, w0[0]), __builtin_fmaf(B(q0, 1), sy, w0[1]),
+                                    __builtin_fmaf(B(q0, 2), sz, w0[2]), 0.f);
+    const float4 l_hi = make_float4(__builtin_fmaf(B(q0, 3), sx, w0[0]), __builtin_fmaf(B(q1, 0), sy, w0[1]),
+                                    __builtin_fmaf(B(q1, 1), sz, w0[2]), 0.f);
+    const float4 r_lo = make_float4(__builtin_fmaf(B(q1, 2), sx, w0[0]), __builtin_fmaf(B(q1, 3), sy, w0[1]),
+                                    __builtin_fmaf(B(q2, 0), sz, w0[2]), 0.f);
+    const float4 r_hi = make_float4(__builtin_fmaf(B(q2, 1), sx, w0[0]), __builtin_fmaf(B(q2, 2), sy, w0[1]),
+                                    __builtin_fmaf(B(q2, 3), sz, w0[2]), 0.f);
+    const uint32_t refs = __float_as_uint(w1[3]);
+    float el = 0.f, er = 0.f;
+    bool pl, pb;
+    if (st.wfast) {   // wave-uniform
+        bool al, ar;
+        pl = aabb_fast(l_lo, l_hi, st.ro, st.rr, el, al);
+        pb = aabb_fast(r_lo, r_hi, st.ro, st.rr, er, ar);
+        if (al | ar) {
+            if (al) pl = aabb_test(l_lo, l_hi, st.ro, st.rd);
+            if (ar) pb = aabb_test(r_lo, r_hi, st.ro, st.rd);
         }
     } else {
-        const int leaf = cur - Q, base = 4 * leaf;
-        if (COUNT) { n_nodes++; n_tris += __float_as_int(sc.hot4[base].c.z); }
-        const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
-        v4f c[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) c[k] = L[k];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
-            const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
-            const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
-            float t, u, v;
-            if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
-                (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
-                st.t_hit = t;
-                st.bu = u;
-                st.bv = v;
-                st.btri = base + i;
-            }
-        }
+        pl = aabb_decide(l_lo, l_hi, st.ro, st.rd, st.rr, st.exact, el);
+        pb = aabb_decide(r_lo, r_hi, st.ro, st.rd, st.rr, st.exact, er);
     }
-    if (!next) {
-        const float tb = st.t_hit;
-        st.cur = -1;
-        while (st.sp > 0) {
-            const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
-            if (!(tb < __uint_as_float(w << 16))) {
-                st.cur = (int)(w >> 16);
-                break;
-            }
-        }
+    const float s = cull_class_size(meta >> 24);
+    const float Tl = cull_threshold(sc, el, s);
+    const float Tr = cull_threshold(sc, er, s);
+    pl = pl && !(t_best < Tl);
+    pb = pb && !(t_best < Tr);
+    const int rl = (int)(refs & 0xffffu), rrf = (int)(refs >> 16);
+    if (pl && pb) {
+        const bool lfirst = el <= er;
+        st.cur = lfirst ? rl : rrf;
+        st.curT = lfirst ? Tl : Tr;
+        const int far = lfirst ? rrf : rl;
+        const float Tf = lfirst ? Tr : Tl;
+        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
+        return true;
     }
+    if (pl | pb) {
+        st.cur = pl ? rl : rrf;
+        st.curT = pl ? Tl : Tr;
+        return true;
+    }
+    return false;
 }
-
+// a leaf entered on its decoded (containing) box: the reference's decision on the leaf's own box
+// (aabb_fast / aabb_decide, as trav_inner takes it on the 64-B layout) before its triangles; the
+// box loads issue with the triangle loads
 template <bool COUNT = false>
-PT_DEV float bvh_intersect_quads(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
-                                 int& btri) {
-    int n_nodes = 0, n_tris = 0;
-    TravState st;
-    trav_begin(sc, st, ro, rd, t_limit);
-    if (st.cur >= 0) st.cur = sc.qroot_ref;
-    while (st.cur >= 0) {
-        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
-        trav_step_quad<COUNT>(sc, st, stack, n_nodes, n_tris);
+PT_DEV void trav_leaf_q(const SceneDev& sc, TravState& st, int leaf, int& n_nodes, int& n_tris) {
+    const int base = 4 * leaf;
+    const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
+    const float4* LB = sc.leafbox + 2 * (size_t)leaf;
+    const float4 lo = LB[0], hi = LB[1];
+    float e;
+    bool pass;
+    if (st.wfast) {
+        bool amb;
+        pass = aabb_fast(lo, hi, st.ro, st.rr, e, amb);
+        if (amb) pass = aabb_test(lo, hi, st.ro, st.rd);
+    } else {
+        pass = aabb_decide(lo, hi, st.ro, st.rd, st.rr, st.exact, e);
     }
+    if (!pass) return;
+    v4f c[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) c[k] = L[k];
     if (COUNT) {
-        sec_add_lanes(SEC_N_NODES, n_nodes);
-        sec_add_lanes(SEC_N_TRIS, n_tris);
-        sec_add_lanes(SEC_N_BVH_RAYS, 1);
+        n_nodes++;
+        n_tris += __float_as_int(sc.hot4[base].c.z);
+        sec_add_lanes(SEC_N_LEAVES, 1);
     }
-    return trav_result(st, bu, bv, btri);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
+        const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
+        const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
+        float t, u, v;
+        if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
+            (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
+            st.t_hit = t;
+            st.bu = u;
+            st.bv = v;
+            st.btri = base + i;
+        }
+    }
+}
+template <bool COUNT = false>
+PT_DEV void trav_step_q(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
+    const int P = sc.num_pairs;
+    bool next = false;
+    if (st.cur < P) {
+        next = trav_inner_q<COUNT>(sc, st, stack, n_nodes);
+    } else {
+        trav_leaf_q<COUNT>(sc, st, st.cur - P, n_nodes, n_tris);
+    }
+    if (!next) trav_pop(st, stack);
 }
 
-template <bool COUNT = false>
+template <bool COUNT = false, bool Q32 = false>
 PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
                                  int& btri) {
     int n_nodes = 0, n_tris = 0;
@@ -695,7 +709,8 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
     if (COUNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
     while (st.cur >= 0) {
         if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
-        trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
+        if (Q32) trav_step_q<COUNT>(sc, st, stack, n_nodes, n_tris);
+        else trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
     }
     if (COUNT) {
         sec_add_lanes(SEC_N_NODES, n_nodes);
