@@ -211,22 +211,6 @@ struct DevPair {
     float4 r_hi;   // right box max.xyz | right cull constants
 };
 
-// VAR_BVH_Q32: DevPair in 32 bytes (two dwordx4 fetches per node expansion instead of four).
-// Both child boxes as 8-bit coordinates on a per-node grid: bound = origin + q * 2^e per axis,
-// computed with one fma that is exact (the host puts the origin on the grid and checks every
-// bound), lows rounded down and highs up -- so each decoded box CONTAINS the child's box.  Inner
-// decisions on containing boxes visit a superset of the reference's inner nodes and, because the
-// reference's slab test is monotone in the bounds, every leaf the reference visits;
-// a leaf is then decided exactly on its own reference box (leafbox) before its triangles count.
-// One cull class for both children: s_q = 2^((c - 128) / 4) >= either child's cull size s.
-struct DevPairQ {
-    float ox, oy, oz;      // grid origin (a multiple of the steps)
-    uint32_t meta;         // bytes 0..2: exponent + 128 of the x / y / z step; byte 3: cull class c
-    uint32_t q[3];         // left lo.xyz, left hi.xyz, right lo.xyz, right hi.xyz: one byte each
-    uint32_t refs;         // left ref | right ref << 16
-};
-static_assert(sizeof(DevPairQ) == 32, "DevPairQ");
-
 // hot triangle record in leaf order (index k = node.start + i): 3 positions, 48 bytes
 struct DevTriHot {
     float4 a;   // v0.xyz, v1.x

@@ -32,8 +32,6 @@ enum : int {
                            // queued and traversed (then shaded) by k_bvh_bounce in full waves
     VAR_BVH_NODES = 64,    // host only: BVH_FAST on the node array instead of the DevPair layout (A/B)
     VAR_BLOCK_REDIST = 128,  // with VAR_WAVE_REDIST: the exchange spans the block (block_intersect)
-    VAR_BVH_Q32 = 256,     // host-set (k_bvh_bounce): the pair layout in 32-B quantized records (DevPairQ)
-                           // for scenes where the node fetches, not the decoding, bind the traversal
     VAR_MAT_GROUP = 512,   // fused MATERIAL_SORTING: the block's paths regrouped by material between
                            // intersection and shading (group_by_material); set by pt_options.material_sort
     VAR_NO_TEX = 1024,     // host-set: no material samples a texture or bump map, so the fused kernels'
@@ -76,8 +74,6 @@ struct SceneDev {
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
-    const DevPairQ* pairq;    // VAR_BVH_Q32 layout (null: not built), same refs as `pairs`
-    const float4* leafbox;    // per leaf: its exact reference box (lo.xyz | -, hi.xyz | -)
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
@@ -579,128 +575,7 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
     return st.t_hit;
 }
 
-// VAR_BVH_Q32: expand st.cur from its 32-B quantized record (DevPairQ).  The decoded boxes contain
-// the children's boxes; the decisions are aabb_fast / aabb_decide's on them (a containing box
-// passes whenever the contained one does), the culls cull_threshold's certified bound for the
-// shared class size.  A leaf child is entered on its decoded box and decided on its own exact
-// box by trav_leaf_q.
-PT_DEV float cull_class_size(uint32_t c) {
-    // 2^(k/4) for k = 0..3, each rounded up to float: s_q >= 2^((c - 128) / 4)
-    const float f = (c & 3) == 0 ? 1.0f : (c & 3) == 1 ? 1.18920720f : (c & 3) == 2 ? 1.41421366f : 1.68179286f;
-    return __builtin_ldexpf(f, (int)(c >> 2) - 32);
-}
 template <bool COUNT = false>
-PT_DEV bool trav_inner_q(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
-    const float t_best = st.t_hit;
-    if (COUNT) n_nodes++;
-    const v4f* R = reinterpret_cast<const v4f*>(sc.pairq + st.cur);
-    const v4f w0 = R[0], w1 = R[1];
-    const uint32_t meta = __float_as_uint(w0[3]);
-    const float sx = __builtin_ldexpf(1.0f, (int)(meta & 255u) - 128);
-    const float sy = __builtin_ldexpf(1.0f, (int)((meta >> 8) & 255u) - 128);
-    const float sz = __builtin_ldexpf(1.0f, (int)((meta >> 16) & 255u) - 128);
-    const uint32_t q0 = __float_as_uint(w1[0]), q1 = __float_as_uint(w1[1]), q2 = __float_as_uint(w1[2]);
-    auto B = [](uint32_t w, int k) { return (float)((w >> (8 * k)) & 255u); };
-    const float4 l_lo = make_float4(__builtin_fmaf(B(q0, 0), sx, w0[0]), __builtin_fmaf(B(q0, 1), sy, w0[1]),
-                                    __builtin_fmaf(B(q0, 2), sz, w0[2]), 0.f);
-    const float4 l_hi = make_float4(__builtin_fmaf(B(q0, 3), sx, w0[0]), __builtin_fmaf(B(q1, 0), sy, w0[1]),
-                                    __builtin_fmaf(B(q1, 1), sz, w0[2]), 0.f);
-    const float4 r_lo = make_float4(__builtin_fmaf(B(q1, 2), sx, w0[0]), __builtin_fmaf(B(q1, 3), sy, w0[1]),
-                                    __builtin_fmaf(B(q2, 0), sz, w0[2]), 0.f);
-    const float4 r_hi = make_float4(__builtin_fmaf(B(q2, 1), sx, w0[0]), __builtin_fmaf(B(q2, 2), sy, w0[1]),
-                                    __builtin_fmaf(B(q2, 3), sz, w0[2]), 0.f);
-    const uint32_t refs = __float_as_uint(w1[3]);
-    float el = 0.f, er = 0.f;
-    bool pl, pb;
-    if (st.wfast) {   // wave-uniform
-        bool al, ar;
-        pl = aabb_fast(l_lo, l_hi, st.ro, st.rr, el, al);
-        pb = aabb_fast(r_lo, r_hi, st.ro, st.rr, er, ar);
-        if (al | ar) {
-            if (al) pl = aabb_test(l_lo, l_hi, st.ro, st.rd);
-            if (ar) pb = aabb_test(r_lo, r_hi, st.ro, st.rd);
-        }
-    } else {
-        pl = aabb_decide(l_lo, l_hi, st.ro, st.rd, st.rr, st.exact, el);
-        pb = aabb_decide(r_lo, r_hi, st.ro, st.rd, st.rr, st.exact, er);
-    }
-    const float s = cull_class_size(meta >> 24);
-    const float Tl = cull_threshold(sc, el, s);
-    const float Tr = cull_threshold(sc, er, s);
-    pl = pl && !(t_best < Tl);
-    pb = pb && !(t_best < Tr);
-    const int rl = (int)(refs & 0xffffu), rrf = (int)(refs >> 16);
-    if (pl && pb) {
-        const bool lfirst = el <= er;
-        st.cur = lfirst ? rl : rrf;
-        st.curT = lfirst ? Tl : Tr;
-        const int far = lfirst ? rrf : rl;
-        const float Tf = lfirst ? Tr : Tl;
-        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
-        return true;
-    }
-    if (pl | pb) {
-        st.cur = pl ? rl : rrf;
-        st.curT = pl ? Tl : Tr;
-        return true;
-    }
-    return false;
-}
-// a leaf entered on its decoded (containing) box: the reference's decision on the leaf's own box
-// (aabb_fast / aabb_decide, as trav_inner takes it on the 64-B layout) before its triangles; the
-// box loads issue with the triangle loads
-template <bool COUNT = false>
-PT_DEV void trav_leaf_q(const SceneDev& sc, TravState& st, int leaf, int& n_nodes, int& n_tris) {
-    const int base = 4 * leaf;
-    const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
-    const float4* LB = sc.leafbox + 2 * (size_t)leaf;
-    const float4 lo = LB[0], hi = LB[1];
-    float e;
-    bool pass;
-    if (st.wfast) {
-        bool amb;
-        pass = aabb_fast(lo, hi, st.ro, st.rr, e, amb);
-        if (amb) pass = aabb_test(lo, hi, st.ro, st.rd);
-    } else {
-        pass = aabb_decide(lo, hi, st.ro, st.rd, st.rr, st.exact, e);
-    }
-    if (!pass) return;
-    v4f c[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] = L[k];
-    if (COUNT) {
-        n_nodes++;
-        n_tris += __float_as_int(sc.hot4[base].c.z);
-        sec_add_lanes(SEC_N_LEAVES, 1);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
-        const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
-        const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
-        float t, u, v;
-        if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
-            (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {
-            st.t_hit = t;
-            st.bu = u;
-            st.bv = v;
-            st.btri = base + i;
-        }
-    }
-}
-template <bool COUNT = false>
-PT_DEV void trav_step_q(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
-    const int P = sc.num_pairs;
-    bool next = false;
-    if (st.cur < P) {
-        next = trav_inner_q<COUNT>(sc, st, stack, n_nodes);
-    } else {
-        trav_leaf_q<COUNT>(sc, st, st.cur - P, n_nodes, n_tris);
-    }
-    if (!next) trav_pop(st, stack);
-}
-
-template <bool COUNT = false, bool Q32 = false>
 PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
                                  int& btri) {
     int n_nodes = 0, n_tris = 0;
@@ -709,8 +584,7 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
     if (COUNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
     while (st.cur >= 0) {
         if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
-        if (Q32) trav_step_q<COUNT>(sc, st, stack, n_nodes, n_tris);
-        else trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
+        trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
     }
     if (COUNT) {
         sec_add_lanes(SEC_N_NODES, n_nodes);

@@ -442,11 +442,9 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #ifndef BVH_WAVES
 #define BVH_WAVES 7
 #endif
-#ifndef BVH_WAVES_Q32
-#define BVH_WAVES_Q32 6
-#endif
+
 template <int VAR>
-__global__ __launch_bounds__(BLOCK, (VAR & VAR_BVH_Q32) ? BVH_WAVES_Q32 : BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
                                                       float* __restrict__ image, int bounce, int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
     const int n = ctl->qcnt[bounce][0];
@@ -470,8 +468,7 @@ __global__ __launch_bounds__(BLOCK, (VAR & VAR_BVH_Q32) ? BVH_WAVES_Q32 : BVH_WA
         float u = 0.f, v = 0.f;
         int tri = -1;
         constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
-        const float tb =
-            bvh_intersect_pairs<CNT, (VAR & VAR_BVH_Q32) != 0>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
+        const float tb = bvh_intersect_pairs<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
         // A.w, B.w and D re-read here (L2): reading every queue word once, before the traversal,
         // keeps 5 more registers live across it -- bunny +6.7 %, khaslana +5.5 % (A/B, round 3)
         const float4 c = q.C[gid], d = q.D[gid];
@@ -893,8 +890,6 @@ struct State {
     DevNode* d_nodes = nullptr;
     DevTriHot* d_hot = nullptr;
     DevPair* d_pairs = nullptr;
-    DevPairQ* d_pairq = nullptr;     // VAR_BVH_Q32 records (pt_init: build_pairq)
-    float4* d_leafbox = nullptr;
     DevTriHot* d_hot4 = nullptr;
     float4* d_leaf9 = nullptr;
     DevTriCold* d_cold = nullptr;
@@ -1029,16 +1024,10 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
            gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
-    // the 32-B records exist for the default traversal variants (and their section-counter forms)
-    constexpr int VB = VAR & ~(VAR_NO_TEX | VAR_SECTION_TIMING);
-    constexpr bool QOK = VB == 50 || VB == 186 || VB == 562 || VB == 698;
-    const size_t bvh_lds = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad;
-    if (SPLIT && QOK && gp->sc.pairq)
-        launch(200 + b, k_bvh_bounce<(QOK ? VAR | VAR_BVH_Q32 : VAR)>, grid, dim3(BLOCK), bvh_lds, gp->sc, gp->queue,
-               out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
-    else if (SPLIT)
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), bvh_lds, gp->sc, gp->queue, out, gp->d_ctl, gp->d_image, b,
-               gp->seg_stride);
+    if (SPLIT)
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
+               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, out, gp->d_ctl,
+               gp->d_image, b, gp->seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1090,9 +1079,7 @@ bool variant_compiled(int v);
 // the fused kernel's template variant for a bounce: the requested bits minus what this bounce /
 // scene does not use
 int effective_variant(bool first, int var) {
-    // host-only bits: layout choices (VAR_BVH_Q32 is applied to the traversal kernel's launch
-    // alone), the texture-free build (below)
-    var &= ~(VAR_BVH_NODES | VAR_NO_TEX | VAR_BVH_Q32);
+    var &= ~(VAR_BVH_NODES | VAR_NO_TEX);   // host-only bits (layout choice; texture-free build: below)
     // camera rays of neighbouring pixels share their candidates: redistribution only costs there
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
@@ -1319,75 +1306,6 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
         if (nd.right >= 0) st.push_back({nd.right, d + 1});
     }
     return h;
-}
-
-// VAR_BVH_Q32 (DevPairQ): each pair's two child boxes on an 8-bit grid of the union box, per
-// axis step 2^e with the origin on the grid, lows rounded down and highs up, every decoded bound
-// checked to be the exact float the device's fma(q, 2^e, origin) gives and to contain the
-// original bound; one cull class for both children rounded up (cull_class_size).  False (the
-// scene keeps the 64-B records) for anything that does not fit.
-float cull_class_size_host(int c) {
-    static const float f[4] = {1.0f, 1.18920720f, 1.41421366f, 1.68179286f};
-    return std::ldexp(f[c & 3], (c >> 2) - 32);
-}
-bool build_pairq(const std::vector<DevPair>& pairs, const std::vector<float>& pair_s, std::vector<DevPairQ>& out) {
-    out.assign(pairs.size(), DevPairQ{});
-    if (pair_s.size() < 2 * pairs.size()) return false;
-    for (size_t i = 0; i < pairs.size(); ++i) {
-        const DevPair& pr = pairs[i];
-        const float lo[2][3] = {{pr.l_lo.x, pr.l_lo.y, pr.l_lo.z}, {pr.r_lo.x, pr.r_lo.y, pr.r_lo.z}};
-        const float hi[2][3] = {{pr.l_hi.x, pr.l_hi.y, pr.l_hi.z}, {pr.r_hi.x, pr.r_hi.y, pr.r_hi.z}};
-        DevPairQ& q = out[i];
-        uint8_t qb[12];
-        uint32_t meta = 0;
-        float org[3];
-        for (int a = 0; a < 3; ++a) {
-            const double ulo = std::min(lo[0][a], lo[1][a]), uhi = std::max(hi[0][a], hi[1][a]);
-            if (!std::isfinite(ulo) || !std::isfinite(uhi) || !(ulo <= uhi)) return false;
-            const double ext = uhi - ulo, mag = std::max({std::fabs(ulo), std::fabs(uhi), 1e-30});
-            int e = std::max(ext > 0 ? (int)std::ceil(std::log2(ext / 254.0)) : -126,
-                             (int)std::ceil(std::log2(mag)) - 23);
-            while (std::ldexp(254.0, e) < ext) ++e;           // log2 rounding
-            if (e < -120 || e > 120) return false;
-            const double step = std::ldexp(1.0, e);
-            const double o = std::floor(ulo / step) * step;
-            if ((double)(float)o != o) return false;
-            org[a] = (float)o;
-            meta |= (uint32_t)(e + 128) << (8 * a);
-            for (int k = 0; k < 2; ++k) {
-                const double ql = std::floor((lo[k][a] - o) / step), qh = std::ceil((hi[k][a] - o) / step);
-                if (!(ql >= 0 && qh <= 255 && ql <= qh)) return false;
-                const double dl = o + ql * step, dh = o + qh * step;
-                if ((double)(float)dl != dl || (double)(float)dh != dh || !(dl <= lo[k][a]) || !(dh >= hi[k][a]))
-                    return false;
-                qb[6 * k + a] = (uint8_t)ql;
-                qb[6 * k + 3 + a] = (uint8_t)qh;
-            }
-        }
-        const float smax = std::max(pair_s[2 * i], pair_s[2 * i + 1]);
-        int c = 0;
-        while (c < 255 && !(cull_class_size_host(c) >= smax)) ++c;
-        if (!(cull_class_size_host(c) >= smax)) return false;      // NaN or beyond the classes
-        meta |= (uint32_t)c << 24;
-        int rl, rr;
-        memcpy(&rl, &pr.l_lo.w, 4);
-        memcpy(&rr, &pr.r_lo.w, 4);
-        if (rl < 0 || rl > 65535 || rr < 0 || rr > 65535) return false;
-        q.ox = org[0];
-        q.oy = org[1];
-        q.oz = org[2];
-        q.meta = meta;
-        for (int w = 0; w < 3; ++w)
-            q.q[w] = (uint32_t)qb[4 * w] | (uint32_t)qb[4 * w + 1] << 8 | (uint32_t)qb[4 * w + 2] << 16 |
-                     (uint32_t)qb[4 * w + 3] << 24;
-        q.refs = (uint32_t)rl | (uint32_t)rr << 16;
-    }
-    return true;
-}
-// which scenes traverse the 32-B records by default (A/B)
-bool q32_default(const pt_scene_view& s) {
-    (void)s;
-    return true;
 }
 
 // The pre-test's candidate table (SceneDev::grid, read by grid_superset): GRID_G^3 origin cells
@@ -1627,7 +1545,7 @@ int ensure_test_paths(int64_t n) {
 void free_all() {
     release_graph();
     free_pass_buffers();
-    void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_pairq, gp->d_leafbox, gp->d_hot4,
+    void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
                     gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -2230,9 +2148,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0;
-    std::vector<float> pair_s;       // cull size s of each pair's left / right child
-    std::vector<DevPairQ> pairq;     // VAR_BVH_Q32 layout (empty: not built)
-    std::vector<float4> leafbox;
+
     float4 pair_root_lo{}, pair_root_hi{};
     double cull_extent = 1.0;
     if (gp->has_bvh) {
@@ -2492,8 +2408,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                             memcpy(&frf, &rf, 4);
                             *lo[k] = make_float4(c.lo[0], c.lo[1], c.lo[2], frf);
                             *hi[k] = make_float4(c.hi[0], c.hi[1], c.hi[2], pack_cull(c.s));
-                            pair_s.resize(2 * (size_t)P);
-                            pair_s[2 * (size_t)i + k] = c.s;
                         }
                     }
                     gp->stack_depth = std::max(gp->stack_depth, th + 1);
@@ -2517,8 +2431,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         memcpy(&frf, &rf, 4);
                         *lo[k] = make_float4(nodes[c].lo.x, nodes[c].lo.y, nodes[c].lo.z, frf);
                         *hi[k] = make_float4(nodes[c].hi.x, nodes[c].hi.y, nodes[c].hi.z, pack_cull(node_aux[c].y));
-                        pair_s.resize(2 * pairs.size());
-                        pair_s[2 * (size_t)id[n] + k] = node_aux[c].y;
                     }
                 }
                 hot4.assign(4 * (size_t)L, DevTriHot{});
@@ -2544,13 +2456,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         }
                         for (int m = 0; m < 9; ++m) (&leaf9[9 * (size_t)k + m].x)[i] = comp9[m];
                     }
-                // VAR_BVH_Q32: the same pairs in 32 B (build_pairq), and each leaf's exact box
-                leafbox.assign(2 * (size_t)L, make_float4(0.f, 0.f, 0.f, 0.f));
-                for (int k = 0; k < L; ++k) {
-                    leafbox[2 * (size_t)k] = nodes[leaf_nodes[k]].lo;
-                    leafbox[2 * (size_t)k + 1] = nodes[leaf_nodes[k]].hi;
-                }
-                if (!build_pairq(pairs, pair_s, pairq)) pairq.clear();
                 if (!sah) gp->pair_depth = height + 1;
                 pair_root_ref = sah ? 0 : ref(0);
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
@@ -2625,15 +2530,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
         RC(upload(gp->d_nodes, nodes.data(), nodes.size()));
         RC(upload(gp->d_hot, hot.data(), hot.size()));
         RC(upload(gp->d_cold, cold.data(), cold.size()));
-        // VAR_BVH_Q32 where the 32-B records pay (build_pairq's note; PT_BVH_Q32=0/1 overrides)
-        static const char* q32_env = getenv("PT_BVH_Q32");
-        const bool q32 = !pairq.empty() && (q32_env ? atoi(q32_env) != 0 : q32_default(*s));
-        if (q32) {
-            RC(dalloc(&gp->d_pairq, pairq.size()));
-            RC(upload(gp->d_pairq, pairq.data(), pairq.size()));
-            RC(dalloc(&gp->d_leafbox, leafbox.size()));
-            RC(upload(gp->d_leafbox, leafbox.data(), leafbox.size()));
-        }
         if (!pairs.empty()) {
             RC(dalloc(&gp->d_pairs, pairs.size()));
             RC(upload(gp->d_pairs, pairs.data(), pairs.size()));
@@ -2699,8 +2595,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.texinfo = gp->d_texinfo;
     sc.num_textures = num_tex;
     sc.pairs = gp->d_pairs;
-    sc.pairq = gp->d_pairq;
-    sc.leafbox = gp->d_leafbox;
     sc.hot4 = gp->d_hot4;
     sc.leaf9 = gp->d_leaf9;
     sc.num_pairs = pair_count;
