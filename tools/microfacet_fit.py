@@ -6,7 +6,7 @@ then compare the Cook-Torrance sphere (interactions.cu:238-435) against them.
                    16x16-pixel tile means of the three images -> tests/golden/microfacet_ref_tiles.npz
   fit   (GPU box)  python tools/microfacet_fit.py fit --out gpurun_out/microfacet_fit.json
                    per image, coordinate descent over the scene parameters the renders differ in
-                   (eye distance, light size and height, sphere size and position) on the tiles whose
+                   (eye distance, field of view, light size / height / emittance, sphere size and position) on the tiles whose
                    pixels do not see the sphere (first hits from pt_test_camera + pt_test_intersect):
                    those tiles are diffuse + emissive light only, both already pinned to the reference
                    (tests/test_ref_renders.py).  200x200 at 256 spp while searching; the best point is
@@ -31,7 +31,8 @@ NT = 50   # tiles per side
 # parameter -> (start, first step, lower, upper)
 PARAMS = {"eye_z": (10.5, 2.0, 4.0, 30.0), "light_s": (3.0, 1.0, 0.5, 9.5), "light_y": (10.0, 0.15, 9.0, 10.0),
           "sphere_s": (4.0, 0.8, 0.5, 8.0), "sphere_y": (4.0, 0.8, 0.5, 8.0), "sphere_x": (0.0, 0.8, -3.0, 3.0),
-          "sphere_z": (0.0, 0.8, -3.0, 3.0), "fovy": (45.0, 5.0, 20.0, 70.0)}
+          "sphere_z": (0.0, 0.8, -3.0, 3.0), "fovy": (45.0, 5.0, 20.0, 70.0), "emit": (10.0, 4.0, 2.0, 60.0),
+          "light_sz": (1.0, 0.25, 0.3, 3.0)}
 
 
 def tiles_of(rgb, n=NT):
@@ -55,9 +56,10 @@ def scene_json(p, metallic, roughness):
     d["Camera"]["EYE"] = [0.0, 5.0, p["eye_z"]]
     d["Camera"]["FOVY"] = p["fovy"]
     d["Materials"]["microfacet_mat"].update({"METALLIC": metallic, "ROUGHNESS": roughness})
+    d["Materials"]["light"]["EMITTANCE"] = p["emit"]
     for o in d["Objects"]:
         if o["MATERIAL"] == "light":
-            o["SCALE"] = [p["light_s"], 0.3, p["light_s"]]
+            o["SCALE"] = [p["light_s"], 0.3, p["light_s"] * p["light_sz"]]
             o["TRANS"] = [0.0, p["light_y"], 0.0]
         if o["MATERIAL"] == "microfacet_mat":
             o["SCALE"] = [p["sphere_s"]] * 3
