@@ -222,6 +222,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     WaveLds* s_wave_isect =
         reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH && !SPLIT ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
     if (lds_geoms) stage_geoms(sc, s_dyn);   // per-lane candidate tests then read their geom from LDS, not L2
+    PT_HOOK(STAGE_EXTRA, lds_geoms, sc, s_dyn);
     const int gid = block_start + tid;
     bool active = gid < n;
     PathReg p;
@@ -2508,12 +2509,15 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     RC(dalloc(&gp->d_mats, mats.size()));
     RC(upload(gp->d_geoms, geoms.data(), geoms.size()));
     RC(dalloc(&gp->d_cull, culls.size()));
-    // the pre-test's candidate table, for scenes whose flat pre-test is long (PT_GRID=0: off, A/B)
+    // the pre-test's candidate table, for scenes whose flat pre-test is long (A/B: PT_GRID=0 off,
+    // PT_GRID=1 also for scenes under GRID_MIN_GEOMS)
     std::vector<unsigned long long> grid;
     float grid_lo[3] = {0.f, 0.f, 0.f}, grid_inv[3] = {0.f, 0.f, 0.f};
     {
-        static const bool grid_off = getenv("PT_GRID") && atoi(getenv("PT_GRID")) == 0;
-        if (!grid_off && s->num_geoms >= GRID_MIN_GEOMS && s->num_geoms <= LDS_GEOMS &&
+        const char* ge = getenv("PT_GRID");
+        const int grid_env = ge ? atoi(ge) : -1;
+        const int grid_min = grid_env == 1 ? 2 : GRID_MIN_GEOMS;
+        if (grid_env != 0 && s->num_geoms >= grid_min && s->num_geoms <= LDS_GEOMS &&
             build_candidate_table(culls, s->num_geoms, s->camera.position, grid, grid_lo, grid_inv)) {
             RC(dalloc(&gp->d_grid, grid.size()));
             RC(upload(gp->d_grid, grid.data(), grid.size()));

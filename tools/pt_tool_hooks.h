@@ -12,6 +12,8 @@
 //   PT_PROBE_EXTRA_LOAD      one more dwordx4 gather of a neighbouring pair record per inner
 //                            traversal step, result kept live (tools/r03_probe.sh)
 //   PT_PROBE_EXTRA_VALU=N    N dependent v_add_f32 per inner traversal step
+//   PT_STAGE_REPS=N          k_bounce stages its LDS geom table N times per block (the price of
+//                            the staging, results unchanged)
 #ifndef PT_TOOL_HOOKS_H
 #define PT_TOOL_HOOKS_H
 
@@ -99,6 +101,19 @@
 #endif
 #else
 #define PT_HOOK_PROBE_INNER(...) ((void)0)
+#endif
+
+#if defined(PT_STAGE_REPS) && PT_STAGE_REPS > 1
+#define PT_HOOK_STAGE_EXTRA(on, sc, s_dyn)                                                      \
+    do {                                                                                        \
+        if (on)                                                                                 \
+            for (int r_ = 1; r_ < PT_STAGE_REPS; ++r_) {                                        \
+                __syncthreads();                                                                \
+                stage_geoms(sc, s_dyn);                                                         \
+            }                                                                                   \
+    } while (0)
+#else
+#define PT_HOOK_STAGE_EXTRA(...) ((void)0)
 #endif
 
 #endif  // PT_TOOL_HOOKS_H
