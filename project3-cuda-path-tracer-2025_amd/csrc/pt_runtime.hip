@@ -1021,9 +1021,11 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     const size_t stack_lds = HAS_BVH && !SPLIT ? gp->bvh_lds : 0;
     // VAR_MAT_GROUP's exchange reuses the exact-test exchange's region (it runs after it)
     const size_t xchg_lds = (VAR & VAR_MAT_GROUP) ? std::max(redist_lds, mat_group_lds(HAS_BVH, false)) : redist_lds;
-    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds, gp->sc, in, out,
-           gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
-    // tools: PT_BVH_LDS_PAD=<bytes> adds unused LDS to the traversal kernel (occupancy A/B)
+    // tools: PT_BOUNCE_LDS_PAD / PT_BVH_LDS_PAD=<bytes> add unused LDS to k_bounce / the traversal
+    // kernel (occupancy A/B)
+    static const size_t bounce_pad = getenv("PT_BOUNCE_LDS_PAD") ? (size_t)atol(getenv("PT_BOUNCE_LDS_PAD")) : 0;
+    launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds + bounce_pad, gp->sc,
+           in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
         launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
@@ -2590,7 +2592,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.stack_depth = gp->stack_depth;
     // the pair traversal pushes at most one entry per level of its hierarchy (never more than the
     // stack_depth the other traversals size their stacks for); k_bvh_bounce's LDS stack is sized
-    // by it -- unless k_bvh_bounce walks the 4-wide layout, which needs stack_depth
+    // by it
     sc.pair_stack_depth = gp->pair_depth > 0 ? std::min(gp->pair_depth, gp->stack_depth) : gp->stack_depth;
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
