@@ -14,6 +14,7 @@
 //   PT_PROBE_EXTRA_VALU=N    N dependent v_add_f32 per inner traversal step
 //   PT_STAGE_REPS=N          k_bounce stages its LDS geom table N times per block (the price of
 //                            the staging, results unchanged)
+//   PT_SLEEP_WAVES=N         k_bounce waves PT_SLEEP_FROM..3 sleep N x 64 cycles after the staging
 #ifndef PT_TOOL_HOOKS_H
 #define PT_TOOL_HOOKS_H
 
@@ -111,6 +112,17 @@
                 __syncthreads();                                                                \
                 stage_geoms(sc, s_dyn);                                                         \
             }                                                                                   \
+    } while (0)
+#elif defined(PT_SLEEP_WAVES)
+// PT_SLEEP_WAVES=N, PT_SLEEP_FROM=w: waves w..3 of every k_bounce block sleep N x 64 cycles after
+// the staging (a stagger / delay probe, results unchanged)
+#ifndef PT_SLEEP_FROM
+#define PT_SLEEP_FROM 0
+#endif
+#define PT_HOOK_STAGE_EXTRA(on, sc, s_dyn)                                                      \
+    do {                                                                                        \
+        if ((threadIdx.x >> 6) >= PT_SLEEP_FROM)                                                \
+            for (int r_ = 0; r_ < PT_SLEEP_WAVES; ++r_) __builtin_amdgcn_s_sleep(1);           \
     } while (0)
 #else
 #define PT_HOOK_STAGE_EXTRA(...) ((void)0)
