@@ -946,23 +946,30 @@ PT_DEV bool certain_exact_miss(const DevGeomHot& g, f3 ro, f3 rd, bool bounded) 
     const int a = g.away_axis;
     return g.type == PT_CUBE && (unsigned)a < 3u && bounded && away_on_axis(g, a, ro, rd);
 }
-// !cull_geom<false>(g) && !certain_exact_miss(g) for every geom, from the DevCull records (same
-// slab arithmetic as cull_geom, same qo / u arithmetic as away_on_axis), as a candidate mask
-// (bit i = geom i).  Records are read four geoms
-// (12 float4, 192 B) at a time, all loads of a group issued before any arithmetic, and the
-// away row is evaluated without a branch (all-zero rows are never "away"), so a group costs
-// one scalar-memory round trip instead of two per geom.  The host pads the record array to a
-// multiple of 4; bits of pad records are masked off by the (wave-uniform) index test.
+// !cull_geom<false>(g) for every geom, from the DevCull records (same slab arithmetic as
+// cull_geom), as a candidate mask (bit i = geom i), minus the one cube the ray certainly leaves
+// (certain_exact_miss).  Records are read four geoms (12 float4, 192 B) at a time through the
+// scalar cache, all loads of a group issued before any arithmetic; the host pads the record array
+// to a multiple of 4, and bits of pad records are masked off by the (wave-uniform) index test.
+// The "away" drop is evaluated for ONE cube per lane: the last kept cube with an away axis whose
+// box holds the ray's origin (t0 <= 0: every slab entry behind the origin) -- the surface a
+// bounce ray leaves.  A ray outside a cube's box that points away from it on an axis already
+// fails the slab test there (axis-aligned boxes), so the drop matters only where the origin is
+// inside; a cube it is not applied to stays a candidate and its exact test rejects it (same
+// results).  Evaluating the row for every kept cube instead cost each wave ~14 instructions per
+// cube, since some lane of the wave keeps nearly every wall.
 #ifndef CULL_GROUP
 #define CULL_GROUP 4
 #endif
 #ifndef XSCAN_BALLOT
 #define XSCAN_BALLOT 1
 #endif
-PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3 rd, bool bounded) {
+PT_DEV uint64_t cull_candidates(const SceneDev& sc, const DevGeomHot* lg, const CullRay& cr, f3 ro, f3 rd,
+                                bool bounded) {
     const float4* rec = reinterpret_cast<const float4*>(sc.cull);
     const int ng = sc.num_geoms;
     uint64_t cand = 0;
+    int og = -1;
     for (int i0 = 0; i0 < ng; i0 += CULL_GROUP) {
         float4 R[3 * CULL_GROUP];
 #pragma unroll
@@ -980,21 +987,12 @@ PT_DEV uint64_t cull_candidates(const SceneDev& sc, const CullRay& cr, f3 ro, f3
                                              __builtin_fmaxf(a2, b2));
             const uint32_t slab = (uint32_t)(t1 >= t0) & (uint32_t)(i0 + k < ng);
             const uint32_t row = (uint32_t)(__float_as_int(C.z) != 0);
-            uint32_t drop = 0;
-            // the away row only where some lane of the wave keeps this cube (wave-uniform branch):
-            // scenes with many geoms skip it for most of them
-            if (__any(slab & row)) {
-                const float qo = (B.z * ro.x + B.w * ro.y) + (C.x * ro.z + C.y * 1.0f);
-                const float u = (B.z * rd.x + B.w * rd.y) + C.x * rd.z;
-                // bitwise, not short-circuit: the compiler would otherwise branch around the row
-                const uint32_t away = ((uint32_t)(qo > 0.5f) & (uint32_t)(u > 0.0f)) |
-                                      ((uint32_t)(qo < -0.5f) & (uint32_t)(u < 0.0f));
-                drop = away & (uint32_t)bounded & row;
-            }
-            bits |= (slab & (drop ^ 1u)) << k;
+            og = (slab & row & (uint32_t)(t0 <= 0.0f)) ? i0 + k : og;
+            bits |= slab << k;
         }
         cand |= (uint64_t)bits << i0;
     }
+    if (og >= 0 && certain_exact_miss(lg[og], ro, rd, bounded)) cand &= ~(1ull << og);
     return cand;
 }
 
@@ -1060,7 +1058,7 @@ PT_DEV void wave_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live, 
         // candidates here, with the same arithmetic, so they take no slot in the exact tests
         const bool bounded = __builtin_fabsf(rd.x) <= 1e3f && __builtin_fabsf(rd.y) <= 1e3f &&
                              __builtin_fabsf(rd.z) <= 1e3f;
-        cand = cull_candidates(sc, cr, ro, rd, bounded);
+        cand = cull_candidates(sc, lg, cr, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);
     int incl = cnt;
@@ -1260,8 +1258,8 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
                              __builtin_fabsf(rd.z) <= 1e3f;
         cand = sc.grid ? cull_candidates_grid(sc, reinterpret_cast<const float4*>(lg + sc.num_geoms), cr, ro, rd,
                                               bounded)
-                       : cull_candidates(sc, cr, ro, rd, bounded);
-        PT_HOOK(DUP_CULL, sc, ro, rd, bounded);
+                       : cull_candidates(sc, lg, cr, ro, rd, bounded);
+        PT_HOOK(DUP_CULL, sc, lg, ro, rd, bounded);
     }
     const int cnt = __builtin_popcountll(cand);
     uint64_t tc1 = 0;

@@ -25,10 +25,10 @@
 #define PT_HOOK(NAME, ...) PT_HOOK_##NAME(__VA_ARGS__)
 
 #if PT_DUP == 1
-#define PT_HOOK_DUP_CULL(sc, ro, rd, bounded)                                                  \
+#define PT_HOOK_DUP_CULL(sc, lg, ro, rd, bounded)                                              \
     do {                                                                                        \
         const f3 ro2_ = ro + mk(0.f, 0.f, 0.f);                                                 \
-        const uint64_t c2_ = cull_candidates(sc, cull_ray(ro2_, rd), ro2_, rd, bounded);        \
+        const uint64_t c2_ = cull_candidates(sc, lg, cull_ray(ro2_, rd), ro2_, rd, bounded);    \
         asm volatile("" ::"v"((uint32_t)c2_), "v"((uint32_t)(c2_ >> 32)));                     \
     } while (0)
 #else
