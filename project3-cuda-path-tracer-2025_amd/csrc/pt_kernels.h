@@ -1027,14 +1027,25 @@ PT_DEV uint64_t cull_candidates_grid(const SceneDev& sc, const float4* lc, const
 PT_DEV int lds_geom_f4(const SceneDev& sc) {
     return sc.num_geoms * ((int)(sizeof(DevGeomHot) / 16) + (sc.grid ? 3 : 0));
 }
+// Every load of a thread's share is issued before any of its LDS stores (a 44-geom table with its
+// pre-test records is 2 float4 per thread: one L2 round trip, not two).  The caller issues the
+// block's path loads before this, so their HBM latency overlaps the table's.
 PT_DEV void stage_geoms(const SceneDev& sc, float4* s_dyn) {
-    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16);
+    constexpr int HOT4 = (int)(sizeof(DevGeomHot) / 16), GEOM4 = (int)(sizeof(DevGeom) / 16), U = 4;
     const float4* src = reinterpret_cast<const float4*>(sc.geoms);
+    const float4* cs = reinterpret_cast<const float4*>(sc.cull);
     const int nh = sc.num_geoms * HOT4;
-    for (int k = threadIdx.x; k < nh; k += BLOCK) s_dyn[k] = src[(k / HOT4) * GEOM4 + k % HOT4];
-    if (sc.grid) {
-        const float4* cs = reinterpret_cast<const float4*>(sc.cull);
-        for (int k = threadIdx.x; k < 3 * sc.num_geoms; k += BLOCK) s_dyn[nh + k] = cs[k];
+    const int n = nh + (sc.grid ? 3 * sc.num_geoms : 0);
+    auto fetch = [&](int k) { return k < nh ? src[(k / HOT4) * GEOM4 + k % HOT4] : cs[k - nh]; };
+    for (int k0 = threadIdx.x; k0 < n; k0 += U * BLOCK) {
+        const int k1 = k0 + BLOCK, k2 = k0 + 2 * BLOCK, k3 = k0 + 3 * BLOCK;
+        // no branch between the loads (indices past the table re-read its last entry)
+        const float4 v0 = fetch(k0), v1 = fetch(min(k1, n - 1)), v2 = fetch(min(k2, n - 1)),
+                     v3 = fetch(min(k3, n - 1));
+        s_dyn[k0] = v0;
+        if (k1 < n) s_dyn[k1] = v1;
+        if (k2 < n) s_dyn[k2] = v2;
+        if (k3 < n) s_dyn[k3] = v3;
     }
     __syncthreads();
 }

@@ -221,8 +221,6 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     int* s_stack = reinterpret_cast<int*>(s_dyn + (lds_geoms ? lds_geom_f4(sc) : 0));
     WaveLds* s_wave_isect =
         reinterpret_cast<WaveLds*>(s_stack + (HAS_BVH && !SPLIT ? sc.stack_depth * BLOCK : 0)) + (tid >> 6);
-    if (lds_geoms) stage_geoms(sc, s_dyn);   // per-lane candidate tests then read their geom from LDS, not L2
-    PT_HOOK(STAGE_EXTRA, lds_geoms, sc, s_dyn);
     const int gid = block_start + tid;
     bool active = gid < n;
     PathReg p;
@@ -259,13 +257,17 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
             }
             p = load_path(in, slot);
         }
-        if (TIMING) {
-            __builtin_amdgcn_s_waitcnt(0);
-            uint64_t t = sec_clock();
-            sec_add(SEC_LOAD, t - tc);
-            sec_add(SEC_N_WAVES, 1);
-            sec_add_lanes(SEC_N_LANES, p.rb > 0 ? 1 : 0);
-        }
+    }
+    // the geom table after the path loads are issued (their latencies overlap); per-lane candidate
+    // tests then read their geom from LDS, not L2
+    if (lds_geoms) stage_geoms(sc, s_dyn);
+    PT_HOOK(STAGE_EXTRA, lds_geoms, sc, s_dyn);
+    if (TIMING && active) {
+        __builtin_amdgcn_s_waitcnt(0);
+        uint64_t t = sec_clock();
+        sec_add(SEC_LOAD, t - tc);
+        sec_add(SEC_N_WAVES, 1);
+        sec_add_lanes(SEC_N_LANES, p.rb > 0 ? 1 : 0);
     }
     bool live = active && p.rb > 0;
     constexpr bool MG = (VAR & VAR_MAT_GROUP) != 0;
@@ -391,7 +393,6 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
     const int tid = threadIdx.x, lane = tid & 63;
     DevGeomHot* s_geoms = reinterpret_cast<DevGeomHot*>(s_dyn);
     BlockLds* s_block = reinterpret_cast<BlockLds*>(s_dyn + lds_geom_f4(sc));
-    stage_geoms(sc, s_dyn);
     const int gid = block_start + tid;
     const bool active = gid < n;
     PathReg p;
@@ -405,6 +406,7 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
         for (int k = 1; k < NSEG; ++k) sofs = (sl == k) ? segoff[k] : sofs;
         p = load_path(in, sl * seg_stride + (gid - sofs));
     }
+    stage_geoms(sc, s_dyn);   // after the path loads are issued
     const int seg = blockIdx.x & (NSEG - 1);
     for (int b = bounce; b < depth; ++b) {
         const bool live = active && p.rb > 0;

@@ -17,3 +17,6 @@ done
 AB_TAG=micro_cornell AB_ROUNDS=4 AB_LIBS="$L" AB_ARGS="--steps 20 --warmup 5" bash tools/ab_libs.sh && \
 AB_TAG=micro_glass AB_ROUNDS=3 AB_LIBS="$L" AB_ARGS="--scene scenes/cornell_glass_test.json --sort --steps 20 --warmup 5" bash tools/ab_libs.sh && \
 AB_TAG=micro_bunny AB_ROUNDS=3 AB_LIBS="$L" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json --steps 20 --warmup 5" bash tools/ab_libs.sh
+[ -n "${AB_KHASLANA:-}" ] && AB_TAG=micro_khaslana AB_ROUNDS=2 AB_LIBS="$L" \
+  AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 20 --warmup 5" bash tools/ab_libs.sh
+exit 0
