@@ -180,6 +180,7 @@ PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i
             tot += c;
         }
         s_b[tid] = tot ? atomicAdd(tid == 0 ? ctr0 : ctr1, tot) : 0;
+        PT_HOOK(ATOMIC_EXTRA, s_b[tid], tid == 0 ? ctr0 : ctr1);
     }
     __syncthreads();
     i0 = s_b[0] + s_w[0][w] + mbcnt(m0);

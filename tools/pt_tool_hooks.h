@@ -15,6 +15,8 @@
 //   PT_STAGE_REPS=N          k_bounce stages its LDS geom table N times per block (the price of
 //                            the staging, results unchanged)
 //   PT_SLEEP_WAVES=N         k_bounce waves PT_SLEEP_FROM..3 sleep N x 64 cycles after the staging
+//   PT_EXTRA_ATOMIC          block_append waits for a second returning atomic (on the counter line's
+//                            padding word) before releasing the block: the price of that latency
 #ifndef PT_TOOL_HOOKS_H
 #define PT_TOOL_HOOKS_H
 
@@ -126,6 +128,18 @@
     } while (0)
 #else
 #define PT_HOOK_STAGE_EXTRA(...) ((void)0)
+#endif
+
+#ifdef PT_EXTRA_ATOMIC
+#define PT_HOOK_ATOMIC_EXTRA(sb, ctr)                                                           \
+    do {                                                                                        \
+        const int x_ = atomicAdd((ctr) + 1, 1);                                                 \
+        int z_;                                                                                 \
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z_) : "v"(x_));                                   \
+        (sb) += z_;                                                                             \
+    } while (0)
+#else
+#define PT_HOOK_ATOMIC_EXTRA(...) ((void)0)
 #endif
 
 #endif  // PT_TOOL_HOOKS_H
