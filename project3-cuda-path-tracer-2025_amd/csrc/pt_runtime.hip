@@ -1761,7 +1761,6 @@ int multi_setup() {
         ShardScope sc(p);
         HIPCHK(hipEventCreateWithFlags(&M.pulled, hipEventDisableTiming));
     }
-    const size_t W = (size_t)p->width;
     for (int k = 1; k < M.n; ++k) {
         State* s = M.shard[k];
         const size_t bytes = 3 * sizeof(float) * (size_t)std::max(1, s->local_pixels);
@@ -1785,7 +1784,6 @@ int multi_setup() {
             RC(dalloc(&M.recv[k], bytes / sizeof(float)));
         }
     }
-    (void)W;
     if (M.combine != PT_COMBINE_RCCL) return PT_OK;
     RC(rccl_open());
     for (int k = 0; k < M.n; ++k) {
