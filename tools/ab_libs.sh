@@ -1,12 +1,12 @@
 #!/usr/bin/env bash
 # A/B two builds of libptamd.so in interleaved processes (same box, same scene):
-#   AB_LIBS="abso/base.so build/libptamd.so" AB_ARGS="--scene scenes/cornell.json" bash tools/ab_libs.sh
+#   AB_LIBS="project3-cuda-path-tracer-2025_amd/build/ab/base.so project3-cuda-path-tracer-2025_amd/build/libptamd.so" AB_ARGS="--scene scenes/cornell.json" bash tools/ab_libs.sh
 # prints ms_per_step per (round, lib) and the per-lib medians; images are not compared here
 # (the GPU parity tests do that for the product build).
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-LIBS=${AB_LIBS:-"abso/base.so project3-cuda-path-tracer-2025_amd/build/libptamd.so"}
+LIBS=${AB_LIBS:-"project3-cuda-path-tracer-2025_amd/build/ab/base.so project3-cuda-path-tracer-2025_amd/build/libptamd.so"}
 ROUNDS=${AB_ROUNDS:-3}
 OUT=gpurun_out/ab_libs_${AB_TAG:-x}.jsonl
 : > "$OUT"

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# A/B of abso/*.so builds on cornell (headline shape), glass, bunny and khaslana (interleaved
-# processes, tools/ab_libs.sh).  Usage: AB_LIBS="abso/a.so abso/b.so" bash tools/r03_ab.sh [scenes]
+# A/B of project3-cuda-path-tracer-2025_amd/build/ab/*.so builds on cornell (headline shape), glass, bunny and khaslana (interleaved
+# processes, tools/ab_libs.sh).  Usage: AB_LIBS="project3-cuda-path-tracer-2025_amd/build/ab/a.so project3-cuda-path-tracer-2025_amd/build/ab/b.so" bash tools/r03_ab.sh [scenes]
 set -u
 cd "$(dirname "$0")/.."
 SC=${1:-"cornell bunny khaslana"}

@@ -23,9 +23,9 @@ if [ "$MODE" = all ] || [ "$MODE" = sections ]; then
 fi
 
 if [ "$MODE" = probe_ab ]; then
-    AB_TAG=probe_bunny AB_ROUNDS=3 AB_LIBS="abso/base.so abso/probe_load.so abso/probe_valu20.so" \
+    AB_TAG=probe_bunny AB_ROUNDS=3 AB_LIBS="project3-cuda-path-tracer-2025_amd/build/ab/base.so project3-cuda-path-tracer-2025_amd/build/ab/probe_load.so project3-cuda-path-tracer-2025_amd/build/ab/probe_valu20.so" \
         AB_ARGS="--steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json" timeout -k 10 600 bash tools/ab_libs.sh || exit 5
-    AB_TAG=probe_khaslana AB_ROUNDS=3 AB_LIBS="abso/base.so abso/probe_load.so abso/probe_valu20.so" \
+    AB_TAG=probe_khaslana AB_ROUNDS=3 AB_LIBS="project3-cuda-path-tracer-2025_amd/build/ab/base.so project3-cuda-path-tracer-2025_amd/build/ab/probe_load.so project3-cuda-path-tracer-2025_amd/build/ab/probe_valu20.so" \
         AB_ARGS="--steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" timeout -k 10 600 bash tools/ab_libs.sh || exit 6
 fi
 echo "probe done"

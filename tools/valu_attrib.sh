@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/valu
 mkdir -p "$OUT"
-for lib in ${VA_LIBS:-abso/new.so abso/dup1.so abso/dup2.so abso/dup3.so abso/dup4.so}; do
+for lib in ${VA_LIBS:-project3-cuda-path-tracer-2025_amd/build/ab/new.so project3-cuda-path-tracer-2025_amd/build/ab/dup1.so project3-cuda-path-tracer-2025_amd/build/ab/dup2.so project3-cuda-path-tracer-2025_amd/build/ab/dup3.so project3-cuda-path-tracer-2025_amd/build/ab/dup4.so}; do
     tag=$(basename "$lib" .so)
     PTAMD_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS \
         -d "$OUT/$tag" -o run --output-format csv -- \
