@@ -80,6 +80,14 @@ def parse():
                     help="N>1: pixels = interleaved row bands of every frame per rank (default); "
                          "samples = whole frames per rank")
     ap.add_argument("--dump-image", default="", help="rank 0 saves the final accumulated image (.npy)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="ONE process driving --gpus N devices behind one pathtrace() (pt_options.num_devices: "
+                         "the path the drop-in and pt_render take), instead of one process per GPU")
+    ap.add_argument("--inproc-devices", default="",
+                    help="--inproc device list, e.g. 0,0 to rehearse on one GPU (default 0..N-1)")
+    ap.add_argument("--combine", choices=["peer", "rccl"], default="peer", help="--inproc: how shards reach device 0")
+    ap.add_argument("--no-inproc", action="store_true",
+                    help="N>1 under torchrun: skip rank 0's follow-up --inproc run of the same N")
     return ap.parse_args()
 
 
@@ -102,9 +110,80 @@ def shard_rows(height: int, world: int) -> int:
     return 1
 
 
+def inproc_main(args):
+    """`--gpus N --inproc`: one process, one PathTracer over N devices (pt_options.num_devices),
+    every frame split into interleaved row bands across them and combined into device 0's image
+    after each call (k_gather_shards over xGMI peer access, or RCCL).  Weak scaling like the
+    torchrun line: K steps of N frames each, so every device traces K frames' worth of paths."""
+    import ptamd   # noqa: E402  (no torch: the library's own HIP runtime)
+    n = args.gpus
+    devices = [int(x) for x in args.inproc_devices.split(",")] if args.inproc_devices else list(range(n))
+    n = len(devices)
+    scene = ptamd.SceneFile(args.scene)
+    tr = ptamd.PathTracer(scene, devices=devices, combine=args.combine)
+    per_step = n
+    it = 1
+    if args.warmup:
+        tr.trace_frames(it, args.warmup * per_step)
+        it += args.warmup * per_step
+    tr.synchronize()
+    tr.reset_stats()
+    tr.prepare_frames(args.steps * per_step)
+    tr.synchronize()
+    t0 = time.perf_counter()
+    tr.trace_frames(it, args.steps * per_step)        # every shard's passes, then one combine
+    tr.synchronize()
+    el = time.perf_counter() - t0
+    it += args.steps * per_step
+    st = tr.stats()
+    assert st["frames_total"] == args.steps * per_step
+    # the API call (one frame per pathtrace(), image copied to host), as main.cpp:463 makes it
+    ts = []
+    for k in range(25):
+        t1 = time.perf_counter()
+        tr.trace(it + k, copy_image=True)
+        if k >= 5:
+            ts.append(1e3 * (time.perf_counter() - t1))
+    ts.sort()
+    tr.free()
+    out = {"metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8", "mode": "inproc",
+           "value": round(st["segments_total"] / el / 1e6, 2), "unit": "Mpaths/s", "n_gpus": n,
+           "devices": devices, "combine": args.combine, "steps": args.steps, "warmup": args.warmup,
+           "frames_per_step": per_step, "ms_per_step": round(1e3 * el / args.steps, 4),
+           "ms_per_frame": round(1e3 * el / (args.steps * per_step), 4),
+           "api_ms_per_frame": round(ts[len(ts) // 2], 4),
+           "parallelism": f"one process, pt_options.num_devices={n}: interleaved 8-row bands per device, "
+                          f"one combine into device 0 per call ({args.combine})"}
+    print(json.dumps(out), flush=True)
+
+
+def inproc_child(args, world):
+    """Rank 0 of a torchrun job, after the other ranks have exited: the same N GPUs once more, as
+    ONE process behind one pathtrace() (--inproc), so the scaling run also times the path the
+    reference's callers get.  A child process with a time limit: its failure is recorded, not fatal."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--inproc", "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--scene", args.scene]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
+                                                              "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 240 s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}", "stderr": p.stderr[-600:]}
+    return json.loads(lines[-1])
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
+    if args.inproc:
+        if env_world is not None and int(env_world) > 1:
+            print("bench.py: --inproc is one process; do not start it under torchrun", file=sys.stderr)
+            sys.exit(2)
+        inproc_main(args)
+        return
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(env_world or "1")
@@ -250,10 +329,12 @@ def main():
             line["configs"] = [sub_config(ptamd, c) for c in SUB_CONFIGS]
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+        if rank == 0 and backend == "nccl" and not args.no_inproc:
+            line["inproc"] = inproc_child(args, world)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
 
 
 def workload_str(name, w, h, depth, sort, pipeline):
@@ -482,6 +563,12 @@ def cpu_baseline(budget_s):
     v1, f1, e1 = run(1, budget_s)
     nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
     vn, fn, en = run(nt, budget_s / 2)
+    # the headline workload itself (BASELINE configs[1], cornell 800x800 depth 8) on the same host,
+    # so the GPU line has a CPU number of the same work beside it: a few frames at 1 thread
+    # (~0.45 s each) and at the process's CPU share
+    sc = O.load_scene(SCENE)
+    h1, hf1, he1 = run(1, budget_s / 2)
+    hn, hfn, hen = run(nt, budget_s / 4)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -493,7 +580,15 @@ def cpu_baseline(budget_s):
                       f"{e1 / f1 * 1e3:.1f} ms/frame, oracle/pt_oracle.c single thread",
             "ms_per_frame": round(e1 / f1 * 1e3, 2),
             "multithread": {"value": round(vn, 3), "unit": "Mpaths/s", "cores": nt,
-                            "sample": f"same workload, {fn} frames in {en:.1f} s, OpenMP over paths"}}
+                            "sample": f"same workload, {fn} frames in {en:.1f} s, OpenMP over paths"},
+            "configs1": {"workload": "cornell.json 800x800 depth 8, stream compaction on (BASELINE configs[1], "
+                                     "the GPU headline's workload)",
+                         "value": round(h1, 3), "unit": "Mpaths/s", "cores": 1,
+                         "ms_per_frame": round(he1 / hf1 * 1e3, 2),
+                         "sample": f"{hf1} frames in {he1:.1f} s, oracle/pt_oracle.c single thread",
+                         "multithread": {"value": round(hn, 3), "unit": "Mpaths/s", "cores": nt,
+                                         "ms_per_frame": round(hen / hfn * 1e3, 2),
+                                         "sample": f"{hfn} frames in {hen:.1f} s, OpenMP over paths"}}}
 
 
 if __name__ == "__main__":

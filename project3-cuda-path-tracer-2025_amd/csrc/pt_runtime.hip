@@ -118,16 +118,6 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
 // Multi-device combine (pt_options.num_devices > 1): shard k owns the pixels
 // shard_pixel_of(sh_k, W, l), l < sh_k.local_pixels, of every shard image; the first device's
 // image receives them after each call.  Plain copies: the image is bit-identical to one device's.
-__global__ __launch_bounds__(BLOCK) void k_pull_shard(float* __restrict__ image, ShardDev sh, int W,
-                                                      const float* __restrict__ src) {   // src: a peer's image
-    const int l = blockIdx.x * BLOCK + threadIdx.x;
-    if (l >= sh.local_pixels) return;
-    const size_t pix = 3 * (size_t)shard_pixel_of(sh, W, l);
-    const float r = src[pix], gch = src[pix + 1], b = src[pix + 2];
-    image[pix] = r;
-    image[pix + 1] = gch;
-    image[pix + 2] = b;
-}
 __global__ __launch_bounds__(BLOCK) void k_pack_tile(const float* __restrict__ image, ShardDev sh, int W,
                                                      float* __restrict__ tile) {
     const int l = blockIdx.x * BLOCK + threadIdx.x;
@@ -137,14 +127,32 @@ __global__ __launch_bounds__(BLOCK) void k_pack_tile(const float* __restrict__ i
     tile[3 * (size_t)l + 1] = image[pix + 1];
     tile[3 * (size_t)l + 2] = image[pix + 2];
 }
-__global__ __launch_bounds__(BLOCK) void k_unpack_tile(float* __restrict__ image, ShardDev sh, int W,
-                                                       const float* __restrict__ tile) {
-    const int l = blockIdx.x * BLOCK + threadIdx.x;
-    if (l >= sh.local_pixels) return;
-    const size_t pix = 3 * (size_t)shard_pixel_of(sh, W, l);
-    image[pix] = tile[3 * (size_t)l];
-    image[pix + 1] = tile[3 * (size_t)l + 1];
-    image[pix + 2] = tile[3 * (size_t)l + 2];
+// The whole combine in ONE launch on the first device: every pixel of the frame finds its shard
+// from its row band ((y / rows) % n) and copies its float3 from that shard's source -- the shard's
+// own image over xGMI peer access (`local` 0: indexed by the global pixel), or the packed tile
+// that RCCL / a peer copy brought over (`local` 1: indexed by the shard's local pixel).  All
+// shards' reads are in flight together (on N GPUs: every xGMI link at once), instead of one
+// launch per shard one after another.  Shard 0's pixels are already in place.
+struct GatherSrc {
+    const float* src[PT_MAX_DEVICES];
+    int local[PT_MAX_DEVICES];
+    int n, rows, W, H;
+};
+__global__ __launch_bounds__(BLOCK) void k_gather_shards(float* __restrict__ image, GatherSrc g) {
+    const int pix = blockIdx.x * BLOCK + threadIdx.x;
+    if (pix >= g.W * g.H) return;
+    const int y = pix / g.W, x = pix - y * g.W;
+    const int band = y / g.rows;
+    const int k = band % g.n;
+    if (k == 0) return;
+    const int lrow = (band / g.n) * g.rows + (y - band * g.rows);
+    const size_t i = 3 * (size_t)(g.local[k] ? lrow * g.W + x : pix);
+    const float* s = g.src[k];
+    const float r = s[i], gch = s[i + 1], b = s[i + 2];
+    float* px = image + 3 * (size_t)pix;
+    px[0] = r;
+    px[1] = gch;
+    px[2] = b;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -925,6 +933,7 @@ struct State {
     int ctl_rows = 1;                // counter rows k_frame_begin folds / clears (max trace depth + 1)
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
+    int* h_cnt = nullptr;            // page-locked copy of the live counters (TracedDepth, frame_depth_*)
     int key_bits = 1;
 };
 State g_primary;                 // the process's context (shard 0 of a multi-device context)
@@ -1556,6 +1565,7 @@ void free_all() {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (gp->stream) (void)hipStreamDestroy(gp->stream);
+    if (gp->h_cnt) (void)hipHostFree(gp->h_cnt);
     int32_t* td = gp->traced_depth;
     *gp = State();
     gp->traced_depth = td;
@@ -1761,11 +1771,15 @@ int multi_setup() {
         ShardScope sc(p);
         HIPCHK(hipEventCreateWithFlags(&M.pulled, hipEventDisableTiming));
     }
+    // tools / tests: PT_COMBINE_FORCE_STAGED=1 sends every PEER shard through its packed tile and a
+    // hipMemcpyPeerAsync (the branch taken without peer access), also when the shards share a device
+    const char* fs = getenv("PT_COMBINE_FORCE_STAGED");
+    const bool force_staged = fs && atoi(fs) != 0;
     for (int k = 1; k < M.n; ++k) {
         State* s = M.shard[k];
         const size_t bytes = 3 * sizeof(float) * (size_t)std::max(1, s->local_pixels);
-        bool direct = M.combine == PT_COMBINE_PEER && s->device == p->device;
-        if (M.combine == PT_COMBINE_PEER && !direct) {
+        bool direct = M.combine == PT_COMBINE_PEER && s->device == p->device && !force_staged;
+        if (M.combine == PT_COMBINE_PEER && !direct && !force_staged) {
             int can = 0;
             if (hipDeviceCanAccessPeer(&can, p->device, s->device) == hipSuccess && can) {
                 ShardScope sc(p);
@@ -1800,6 +1814,16 @@ int multi_setup() {
     }
     HIPCHK(hipSetDevice(p->device));
     return PT_OK;
+}
+
+// k_gather_shards' shard layout (sources filled in by the caller)
+GatherSrc gather_src(int W, int H) {
+    GatherSrc g{};
+    g.n = M.n;
+    g.rows = std::max(1, M.shard[0]->sc.shard.rows);
+    g.W = W;
+    g.H = H;
+    return g;
 }
 
 // every shard's pixels into the first device's image, ordered after the work queued so far on
@@ -1847,28 +1871,35 @@ int multi_combine() {
         }
         ShardScope sc(p);
         HIPCHK(hipStreamWaitEvent(p->stream, M.cdone[d0], 0));
+        // every shard's own work too (its TracedDepth counter copy is queued before done[k]):
+        // once the first device's stream has drained, so has every shard's frame
+        for (int k = 1; k < M.n; ++k) HIPCHK(hipStreamWaitEvent(p->stream, M.done[k], 0));
+        GatherSrc g = gather_src(W, p->height);
         for (int k = 1; k < M.n; ++k) {
-            hipLaunchKernelGGL(k_unpack_tile, dim3(nblocks(M.shard[k]->local_pixels)), dim3(BLOCK), 0, p->stream,
-                               p->d_image, M.shard[k]->sc.shard, W, (const float*)M.recv[k]);
-            HIPCHK(hipGetLastError());
+            g.src[k] = M.recv[k];
+            g.local[k] = 1;
         }
+        hipLaunchKernelGGL(k_gather_shards, dim3(nblocks(p->pixels_total)), dim3(BLOCK), 0, p->stream, p->d_image, g);
+        HIPCHK(hipGetLastError());
         return PT_OK;
     }
     ShardScope sc(p);
+    GatherSrc g = gather_src(W, p->height);
     for (int k = 1; k < M.n; ++k) {
         State* s = M.shard[k];
         HIPCHK(hipStreamWaitEvent(p->stream, M.done[k], 0));
-        if (M.direct[k]) {
-            hipLaunchKernelGGL(k_pull_shard, dim3(nblocks(s->local_pixels)), dim3(BLOCK), 0, p->stream, p->d_image,
-                               s->sc.shard, W, (const float*)s->d_image);
-        } else {
+        if (M.direct[k]) {   // read in place over peer access
+            g.src[k] = s->d_image;
+            g.local[k] = 0;
+        } else {             // packed tile, copied to the first device
             HIPCHK(hipMemcpyPeerAsync(M.recv[k], p->device, M.tile[k], s->device,
                                       3 * sizeof(float) * (size_t)s->local_pixels, p->stream));
-            hipLaunchKernelGGL(k_unpack_tile, dim3(nblocks(s->local_pixels)), dim3(BLOCK), 0, p->stream, p->d_image,
-                               s->sc.shard, W, (const float*)M.recv[k]);
+            g.src[k] = M.recv[k];
+            g.local[k] = 1;
         }
-        HIPCHK(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_gather_shards, dim3(nblocks(p->pixels_total)), dim3(BLOCK), 0, p->stream, p->d_image, g);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(M.pulled, p->stream));
     for (int k = 1; k < M.n; ++k) {   // a shard's image changes again only after it was read
         ShardScope s2(M.shard[k]);
@@ -1878,21 +1909,26 @@ int multi_combine() {
 }
 
 // GuiDataContainer::TracedDepth of the last single-frame pass of the current context: the loop
-// stops after bounce k when no path is left alive, or at traceDepth (pathtrace.cu:759-770)
-int frame_depth(int& depth) {
-    depth = std::max(1, gp->sc.trace_depth);
+// stops after bounce k when no path is left alive, or at traceDepth (pathtrace.cu:759-770).
+// Two halves so that no call waits twice: frame_depth_enqueue queues the copy of the frame's live
+// counters into page-locked host memory on the context's stream (behind the frame, before the
+// caller's one synchronisation), frame_depth_read reads them after it.
+int frame_depth_enqueue() {
     if (!gp->opts.stream_compaction) return PT_OK;
-    std::vector<int> cnt((size_t)depth * NSEG * CNT_PAD);
-    HIPCHK(smemcpy(cnt.data(), &gp->d_ctl->cnt[0][0][0], cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+    const size_t n = (size_t)std::max(1, gp->sc.trace_depth) * NSEG * CNT_PAD;
+    if (!gp->h_cnt) HIPCHK(hipHostMalloc((void**)&gp->h_cnt, sizeof(int) * (size_t)(MAXB + 1) * NSEG * CNT_PAD));
+    HIPCHK(hipMemcpyAsync(gp->h_cnt, &gp->d_ctl->cnt[0][0][0], n * sizeof(int), hipMemcpyDeviceToHost, gp->stream));
+    return PT_OK;
+}
+int frame_depth_read() {
+    int depth = std::max(1, gp->sc.trace_depth);
+    if (!gp->opts.stream_compaction || !gp->h_cnt) return depth;
     for (int k = 1; k < depth; ++k) {
         int64_t live = 0;
-        for (int q = 0; q < NSEG; ++q) live += cnt[((size_t)k * NSEG + q) * CNT_PAD];
-        if (live == 0) {
-            depth = k;
-            break;
-        }
+        for (int q = 0; q < NSEG; ++q) live += gp->h_cnt[((size_t)k * NSEG + q) * CNT_PAD];
+        if (live == 0) return k;
     }
-    return PT_OK;
+    return depth;
 }
 
 }  // namespace
@@ -1956,16 +1992,16 @@ int32_t pt_free(void) {
         multi_release();
         for (int k = M.n - 1; k >= 1; --k) {
             if (!M.shard[k]) continue;
-            {
+            {   // whatever a shard allocated, also when its init_one failed part-way (inited false):
+                // free_all releases only the buffers and stream that exist
                 ShardScope sc(M.shard[k]);
-                if (gp->inited) free_all();
+                free_all();
             }
             delete M.shard[k];
         }
     }
     M = Multi();
-    if (gp->inited) free_all();
-    gp->inited = false;
+    free_all();   // also resets g_primary's sizes (alloc_frames, capacity, ...) after a failed init
     return PT_OK;
 }
 
@@ -2714,6 +2750,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         RC(run_frame(iteration));
+        if (g_primary.traced_depth) RC(frame_depth_enqueue());   // read after the one sync below
     }
     RC(multi_combine());
     if (pbo) {
@@ -2729,6 +2766,8 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
         HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
     }
+    // one wait: the first device's stream waited for every shard's frame (multi_combine), and each
+    // shard queued its counter copy before that
     HIPCHK(hipStreamSynchronize(gp->stream));
     if (gp->traced_depth) {
         // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770); with
@@ -2736,9 +2775,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         int depth = 0;
         for (int k = 0; k < nshards(); ++k) {
             ShardScope sc(shard_ctx(k));
-            int d = 0;
-            RC(frame_depth(d));
-            depth = std::max(depth, d);
+            depth = std::max(depth, frame_depth_read());
         }
         *gp->traced_depth = depth;
     }

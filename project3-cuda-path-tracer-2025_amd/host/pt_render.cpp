@@ -144,7 +144,14 @@ int main(int argc, char** argv) {
             } else {
                 for (size_t s = 0; s <= d.size() && opts.num_devices < PT_MAX_DEVICES;) {
                     const size_t e = std::min(d.find(',', s), d.size());
-                    opts.device_ids[opts.num_devices++] = std::atoi(d.substr(s, e - s).c_str());
+                    const std::string tok = d.substr(s, e - s);
+                    char* end = nullptr;
+                    const long v = std::strtol(tok.c_str(), &end, 10);
+                    if (tok.empty() || *end != '\0' || v < 0) {   // "0,,1", "0,1,", "0,x"
+                        std::fprintf(stderr, "--devices: bad device id '%s' in '%s'\n", tok.c_str(), d.c_str());
+                        return 2;
+                    }
+                    opts.device_ids[opts.num_devices++] = (int32_t)v;
                     s = e + 1;
                 }
             }

@@ -150,6 +150,38 @@ def test_multi_device_passes_bitexact(name, res, devices, combine, fpp, oracle, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,res,devices,opts", [
+    ("cornell", (64, 64), [0, 0], {}),
+    ("cornell_glass_test", (64, 48), [0, 0, 0, 0], {"material_sort": 1}),
+    ("cornell_obj_bnnuy", (64, 56), [0, 0, 0], {"shard_rows": 4}),
+])
+def test_multi_device_staged_peer_combine_bitexact(name, res, devices, opts, oracle, ptamd, monkeypatch):
+    """the PEER combine's branch for a shard the first device cannot read in place
+    (no peer access): k_pack_tile on the shard's stream -> hipMemcpyPeerAsync -> the one
+    k_gather_shards launch reading the packed tiles.  PT_COMBINE_FORCE_STAGED=1 takes it although
+    the shards share device 0; API frames (TracedDepth, host copy) and multi-frame passes."""
+    monkeypatch.setenv("PT_COMBINE_FORCE_STAGED", "1")
+    a, b = _pair(oracle, ptamd, name, res)
+    td = ctypes.c_int32(-7)
+    ptamd.lib.pt_init_data_container(ctypes.byref(td))
+    tr = ptamd.PathTracer(b, devices=devices, combine="peer", **opts)
+    r = oracle.Renderer(a, oracle.options(material_sort=opts.get("material_sort", 0), **BIT))
+    try:
+        for it in (1, 2):
+            live = r.trace(it)
+            img = tr.trace(it, copy_image=True)
+            assert _eq(img, r.image), it
+            assert td.value == next((k for k in range(1, a.trace_depth) if live[k] <= 0), a.trace_depth)
+        for it in range(3, 8):
+            r.trace(it)
+        tr.trace_frames(3, 5)
+        assert _eq(tr.image(), r.image)
+    finally:
+        tr.free()
+        ptamd.lib.pt_init_data_container(None)
+
+
+@pytest.mark.gpu
 def test_multi_device_equals_single_device_full_resolution(ptamd):
     """BASELINE configs[1] (cornell 800x800 d8): 8 shard contexts == one context, bit for bit."""
     b = ptamd.SceneFile(scene_path("cornell"))

@@ -45,6 +45,26 @@ def api(ptamd, sc, frames=40, **opts):
     return round(1e3 * dt, 4)
 
 
+def enqueue(ptamd, sc, f, calls=20, **opts):
+    """host microseconds per shard for pt_trace_frames(., f) to RETURN (the passes' launches or
+    graph replays and the combine's enqueue, no wait): the serial host walk over the shards"""
+    tr = ptamd.PathTracer(sc, **opts)
+    n = len(opts.get("devices") or [0])
+    tr.trace_frames(1, 2 * f)
+    tr.prepare_frames(f)
+    tr.synchronize()
+    ts = []
+    for c in range(calls):
+        tr.synchronize()
+        t0 = time.perf_counter()
+        tr.trace_frames(1 + (2 + c) * f, f)
+        ts.append(time.perf_counter() - t0)
+    tr.synchronize()
+    tr.free()
+    ts.sort()
+    return round(1e6 * ts[len(ts) // 2] / n, 1)
+
+
 def main():
     import ptamd
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 20
@@ -56,6 +76,11 @@ def main():
         key = f"{n} shards on device 0, {comb}"
         out["passes"][key] = passes(ptamd, sc, k, devices=[0] * n, combine=comb)
         out["api"][key] = api(ptamd, sc, devices=[0] * n, combine=comb)
+    out["enqueue_us_per_shard"] = {}
+    for n in (1, 2, 8):
+        for f in (1, 20):
+            kw = {} if n == 1 else {"devices": [0] * n}
+            out["enqueue_us_per_shard"][f"{n} shard(s), F={f}"] = enqueue(ptamd, sc, f, **kw)
     print(json.dumps(out))
 
 

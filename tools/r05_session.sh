@@ -1,0 +1,34 @@
+#!/usr/bin/env bash
+# Round-5 GPU session: tools/r05_session.sh STEP...
+# Each step has its own time limit; a failure other than test failures stops the session.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {   # step NAME TIMEOUT CMD...
+    local name=$1 to=$2; shift 2
+    echo "== $name (timeout ${to}s) =="
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    tail -n 5 "$OUT/$name.log"
+    echo "== $name rc=$rc =="
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
+    return 0
+}
+PYT="python -u -m pytest -x -q -rf --timeout 200 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+    case $s in
+        new) step pytest_new 500 $PYT tests/test_multi_device.py tests/test_dropin.py -m gpu ;;
+        glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
+        mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
+        gpu) step pytest_gpu 900 $PYT tests -m gpu ;;
+        smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) step bench_k20 400 python bench.py --steps 20 --warmup 5 ;;
+        benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
+        multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
+        inproc) step inproc 200 python bench.py --gpus 2 --inproc --inproc-devices 0,0 --steps 20 --warmup 5 ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "session done"
