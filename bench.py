@@ -115,6 +115,7 @@ def inproc_main(args):
     every frame split into interleaved row bands across them and combined into device 0's image
     after each call (k_gather_shards over xGMI peer access, or RCCL).  Weak scaling like the
     torchrun line: K steps of N frames each, so every device traces K frames' worth of paths."""
+    sys.path.insert(0, PKG)
     import ptamd   # noqa: E402  (no torch: the library's own HIP runtime)
     n = args.gpus
     devices = [int(x) for x in args.inproc_devices.split(",")] if args.inproc_devices else list(range(n))

@@ -105,7 +105,11 @@ struct FrameCtl {
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     unsigned long long qtot[MAXB + 1];      // the same for qcnt (paths of bounce b queued for traversal)
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
-    int qcnt[MAXB + 1][CNT_PAD];            // VAR_BVH_SPLIT: paths of bounce b queued for traversal
+    // VAR_BVH_SPLIT: paths of bounce b queued for traversal, per queue segment (blockIdx % NSEG of
+    // the queuing k_bounce block).  One counter per segment, not one for the whole queue: every
+    // block's returning atomic on ONE word serialised at the memory side (~88 / us, the guide's
+    // 'dequeue' row) -- 43k blocks per launch put a ~0.5 ms floor under k_bounce in mesh scenes
+    int qcnt[MAXB + 1][NSEG][CNT_PAD];
 };
 
 // VAR_SECTION_TIMING (tools/section_times.py): wave-level s_memtime deltas per kernel section and

@@ -53,12 +53,14 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
             unsigned long long s = 0;
             for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k][0];
             ctl->tot[b] += s;
-            ctl->qtot[b] += (unsigned)ctl->qcnt[b][0];
+            unsigned long long q = 0;
+            for (int k = 0; k < NSEG; ++k) q += (unsigned)ctl->qcnt[b][k][0];
+            ctl->qtot[b] += q;
         }
     }
     __syncthreads();
     for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->cnt[0][0][0])[i * CNT_PAD] = 0;
-    for (int i = t; i < rows; i += blockDim.x) ctl->qcnt[i][0] = 0;
+    for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
@@ -160,13 +162,56 @@ __global__ __launch_bounds__(BLOCK) void k_gather_shards(float* __restrict__ ima
 // --------------------------------------------------------------------------------------------
 // VAR_BVH_SPLIT traversal queue: the path (3 float4 as in PathBuf, C.w = frame slot | (winner
 // geom + 1) << 8) and the primitive result it enters traversal with (t_min, normal seed)
+// PT_QIDX (A/B): the entry names the path instead of copying it -- E = (source, winner geom + 1),
+// D as above -- and k_bvh_bounce gathers the path from the bounce's input segments (read-only
+// while the bounce runs) or, at bounce 0, regenerates the camera ray from its index: 24 B written
+// per queued ray instead of 64
+#ifndef PT_QIDX
+#define PT_QIDX 0
+#endif
 struct QueueBuf {
     float4 *A, *B, *C, *D;   // D = t_min | seed.xyz
+    int2* E;                 // PT_QIDX: source (camera path index at bounce 0, else input slot) | winner + 1
+    int stride;              // entries per queue segment (segment s at s * stride, FrameCtl::qcnt)
 };
+// queue entry k for path p (read from input slot / camera index `src`) and its primitive result
+PT_DEV void queue_put(const QueueBuf& q, int k, const PathReg& p, int src, float qt, int qw, f3 qs) {
+    q.D[k] = make_float4(qt, qs.x, qs.y, qs.z);
+    if (PT_QIDX) {
+        q.E[k] = make_int2(src, qw + 1);
+    } else {
+        q.A[k] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+        q.B[k] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+        q.C[k] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
+    }
+}
 
 // Block-aggregated append of up to two flags: ballot -> per-wave counts -> one atomic per flag
 // per block (counters on their own cache lines).  Returns each flagged lane's index.  Every
 // thread of the block must call it.
+// Slot of the gid-th entry of a segmented buffer: segment s holds entries [segoff[s], segoff[s+1])
+// at s * stride.  Resolved once per wave on the scalar unit; per lane only if the wave straddles a
+// segment boundary (at most NSEG-1 waves per launch).
+PT_DEV int segment_slot(const int* segoff, int gid, int block_start, int stride) {
+    const int w0 = block_start + (__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6) << 6);
+    int lo = 0, hi = segoff[1], sb = 0;
+#pragma unroll
+    for (int k = 1; k < NSEG; ++k)
+        if (w0 >= segoff[k]) {
+            lo = segoff[k];
+            hi = segoff[k + 1];
+            sb = k;
+        }
+    if (w0 + 63 < hi) return sb * stride - lo + gid;
+    int sl = 0;
+#pragma unroll
+    for (int k = 1; k < NSEG; ++k) sl += (gid >= segoff[k]) ? 1 : 0;
+    int sofs = 0;
+#pragma unroll
+    for (int k = 1; k < NSEG; ++k) sofs = (sl == k) ? segoff[k] : sofs;
+    return sl * stride + (gid - sofs);
+}
+
 template <bool TWO>
 PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i1) {
     __shared__ int s_w[2][BLOCK / 64];
@@ -195,8 +240,22 @@ PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i
     i1 = TWO ? s_b[1] + s_w[1][w] + mbcnt(m1) : 0;
 }
 
+// Scalar registers decide how many 256-thread blocks a CU admits, beside VGPRs and LDS:
+// min(8, floor(800 / (ceil(sgpr / 16) * 16 + 16))) (MI355X_MICROARCH.md, Residency) -- 80 SGPRs
+// for 8 blocks, 96 for 7, 112 for 6.  The compiler's occupancy model does not count this, so a
+// kernel whose uniform state grows past 80 SGPRs silently loses blocks.  PT_KB_NUM_SGPR caps
+// k_bounce's (0: no cap).
+#ifndef PT_KB_NUM_SGPR
+#define PT_KB_NUM_SGPR 0
+#endif
+#if PT_KB_NUM_SGPR > 0
+#define PT_KB_SGPR_ATTR __attribute__((amdgpu_num_sgpr(PT_KB_NUM_SGPR)))
+#else
+#define PT_KB_SGPR_ATTR
+#endif
+
 template <bool FIRST, bool HAS_BVH, int VAR>
-__global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride,
                                                   QueueBuf q) {
     // dynamic LDS: [geom table, sc.num_geoms <= LDS_GEOMS, candidate-queue variants]
@@ -234,37 +293,15 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     bool active = gid < n;
     PathReg p;
     p.rb = 0;
+    int src = gid;   // where k_bvh_bounce finds this path again (PT_QIDX): camera index / input slot
     if (active) {
         if (FIRST) {
             const int slot = gid / sc.shard.local_pixels;
             p = camera_ray(sc.cam, iter + slot, sc.trace_depth, shard_pixel(sc, gid - slot * sc.shard.local_pixels));
             p.slot = slot;
         } else {
-            // input slot of live path gid: segment s holds [segoff[s], segoff[s+1]) at s*seg_stride.
-            // Resolved once per wave on the scalar unit; per lane only if the wave straddles a
-            // segment boundary (at most NSEG-1 waves per bounce).
-            const int w0 = block_start + (__builtin_amdgcn_readfirstlane(tid >> 6) << 6);
-            int lo = 0, hi = segoff[1], sb = 0;
-#pragma unroll
-            for (int k = 1; k < NSEG; ++k)
-                if (w0 >= segoff[k]) {
-                    lo = segoff[k];
-                    hi = segoff[k + 1];
-                    sb = k;
-                }
-            int slot;
-            if (w0 + 63 < hi) {
-                slot = sb * seg_stride - lo + gid;
-            } else {
-                int sl = 0;
-#pragma unroll
-                for (int k = 1; k < NSEG; ++k) sl += (gid >= segoff[k]) ? 1 : 0;
-                int sofs = 0;
-#pragma unroll
-                for (int k = 1; k < NSEG; ++k) sofs = (sl == k) ? segoff[k] : sofs;
-                slot = sl * seg_stride + (gid - sofs);
-            }
-            p = load_path(in, slot);
+            src = segment_slot(segoff, gid, block_start, seg_stride);
+            p = load_path(in, src);
         }
     }
     // the geom table after the path loads are issued (their latencies overlap); per-lane candidate
@@ -319,12 +356,10 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     if (MG) {   // MATERIAL_SORTING: regroup the block's paths by material, then shade
         if (SPLIT) {   // the rays queued for the mesh leave first, from their own threads
             int qi, unused;
-            block_append<false>(queued, &ctl->qcnt[bounce][0], false, nullptr, qi, unused);
+            block_append<false>(queued, &ctl->qcnt[bounce][blockIdx.x & (NSEG - 1)][0], false, nullptr, qi, unused);
+            qi += (blockIdx.x & (NSEG - 1)) * q.stride;
             if (queued) {
-                q.A[qi] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
-                q.B[qi] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
-                q.C[qi] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
-                q.D[qi] = make_float4(qt, qs.x, qs.y, qs.z);
+                queue_put(q, qi, p, src, qt, qw, qs);
                 active = false;   // handed over to k_bvh_bounce
                 live = false;
                 queued = false;
@@ -353,28 +388,21 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
         const uint64_t mq = __ballot(queued);
         if (mq != 0) {
             int base = 0;
-            if (lane == 0) base = atomicAdd(&ctl->qcnt[bounce][0], __popcll(mq));
+            if (lane == 0) base = atomicAdd(&ctl->qcnt[bounce][seg][0], __popcll(mq));
             base = __shfl(base, 0);
             if (queued) {
-                const int k = base + mbcnt(mq);
-                q.A[k] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
-                q.B[k] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
-                q.C[k] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
-                q.D[k] = make_float4(qt, qs.x, qs.y, qs.z);
+                const int k = seg * q.stride + base + mbcnt(mq);
+                queue_put(q, k, p, src, qt, qw, qs);
             }
         }
         return;
     }
     // block-aggregated compaction (+ the traversal queue): one atomic per counter per block
     int si, qi;
-    block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][0], si, qi);
+    block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
     if (surv) store_path(out, seg * seg_stride + si, p);
-    if (SPLIT && queued) {
-        q.A[qi] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
-        q.B[qi] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
-        q.C[qi] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
-        q.D[qi] = make_float4(qt, qs.x, qs.y, qs.z);
-    }
+    qi += seg * q.stride;
+    if (SPLIT && queued) queue_put(q, qi, p, src, qt, qw, qs);
     if (TIMING && active) sec_add(SEC_STORE, sec_clock() - tc);
 }
 
@@ -455,11 +483,16 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #define BVH_WAVES 7
 #endif
 
-template <int VAR>
-__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
-                                                      float* __restrict__ image, int bounce, int seg_stride) {
+template <bool FIRST, int VAR>
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf in, PathBuf out,
+                                                                 FrameCtl* ctl, float* __restrict__ image, int bounce,
+                                                                 int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
-    const int n = ctl->qcnt[bounce][0];
+    int segoff[NSEG + 1];
+    segoff[0] = 0;
+#pragma unroll
+    for (int s = 0; s < NSEG; ++s) segoff[s + 1] = segoff[s] + ctl->qcnt[bounce][s][0];
+    const int n = segoff[NSEG];
     const int block_start = blockIdx.x * BLOCK;
     if (block_start >= n) return;
     int* s_stack = reinterpret_cast<int*>(s_dyn);
@@ -471,25 +504,60 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     PathReg p;
     p.rb = 0;
     if (active) {
-        // traversal needs only the ray and its primitive t; the rest of the queue entry is
-        // fetched afterwards (fewer registers live across the traversal loop -> occupancy)
-        const float4 a = q.A[gid], b = q.B[gid];
-        const float t_prim = q.D[gid].x;
-        p.o = mk(a.x, a.y, a.z);
-        p.d = mk(b.x, b.y, b.z);
+        // traversal needs only the ray and its primitive t; the rest of the path is fetched
+        // afterwards (fewer registers live across the traversal loop -> occupancy)
+        const int qs = segment_slot(segoff, gid, block_start, q.stride);
+        const float t_prim = q.D[qs].x;
+        if (PT_QIDX) {
+            const int src = q.E[qs].x;
+            if (FIRST) {   // the camera ray again, from its path index (bit-identical: same function)
+                const int slot = src / sc.shard.local_pixels;
+                const PathReg c = camera_ray(sc.cam, iter + slot, sc.trace_depth,
+                                             shard_pixel(sc, src - slot * sc.shard.local_pixels));
+                p.o = c.o;
+                p.d = c.d;
+            } else {
+                const float4 a = in.A[src], b = in.B[src];
+                p.o = mk(a.x, a.y, a.z);
+                p.d = mk(b.x, b.y, b.z);
+            }
+        } else {
+            const float4 a = q.A[qs], b = q.B[qs];
+            p.o = mk(a.x, a.y, a.z);
+            p.d = mk(b.x, b.y, b.z);
+        }
         float u = 0.f, v = 0.f;
         int tri = -1;
         constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
         const float tb = bvh_intersect_pairs<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
-        // A.w, B.w and D re-read here (L2): reading every queue word once, before the traversal,
+        // the other words re-read here (L2): reading every word once, before the traversal,
         // keeps 5 more registers live across it -- bunny +6.7 %, khaslana +5.5 % (A/B, round 3)
-        const float4 c = q.C[gid], d = q.D[gid];
-        p.pix = __float_as_int(q.A[gid].w);
-        p.rb = __float_as_int(q.B[gid].w);
-        p.c = mk(c.x, c.y, c.z);
-        const int cw = __float_as_int(c.w);
-        p.slot = cw & 255;
-        const int win = (cw >> 8) - 1;
+        const float4 d = q.D[qs];
+        int win;
+        if (PT_QIDX) {
+            const int2 e = q.E[qs];
+            win = e.y - 1;
+            if (FIRST) {
+                p.slot = e.x / sc.shard.local_pixels;
+                p.pix = shard_pixel(sc, e.x - p.slot * sc.shard.local_pixels);
+                p.rb = sc.trace_depth;
+                p.c = mk(1.f, 1.f, 1.f);
+            } else {
+                const float4 c = in.C[e.x];
+                p.pix = __float_as_int(in.A[e.x].w);
+                p.rb = __float_as_int(in.B[e.x].w);
+                p.c = mk(c.x, c.y, c.z);
+                p.slot = __float_as_int(c.w);
+            }
+        } else {
+            const float4 c = q.C[qs];
+            p.pix = __float_as_int(q.A[qs].w);
+            p.rb = __float_as_int(q.B[qs].w);
+            p.c = mk(c.x, c.y, c.z);
+            const int cw = __float_as_int(c.w);
+            p.slot = cw & 255;
+            win = (cw >> 8) - 1;
+        }
         const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
         shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
@@ -1040,9 +1108,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
            in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
-               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, out, gp->d_ctl,
-               gp->d_image, b, gp->seg_stride);
+        launch(200 + b, k_bvh_bounce<FIRST, VAR>, grid, dim3(BLOCK),
+               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, in, out,
+               gp->d_ctl, gp->d_image, b, gp->seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1468,6 +1536,7 @@ void free_pass_buffers() {
     dfree(gp->queue.B);
     dfree(gp->queue.C);
     dfree(gp->queue.D);
+    dfree(gp->queue.E);
     dfree(gp->d_contrib);
     gp->sc.contrib = nullptr;
     gp->alloc_frames = 0;
@@ -1481,6 +1550,11 @@ int seg_stride_for(int frames) {
     const int nb = nblocks(std::max(1, gp->local_pixels * frames));
     return ((nb + NSEG - 1) / NSEG) * BLOCK * (gp->split ? 2 : 1);
 }
+// entries per traversal-queue segment: the rays of its k_bounce blocks (blockIdx % NSEG)
+int q_stride_for(int frames) {
+    const int nb = nblocks(std::max(1, gp->local_pixels * frames));
+    return ((nb + NSEG - 1) / NSEG) * BLOCK;
+}
 // paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
 int capacity_for(int frames) {
     const int c = std::max(seg_stride_for(frames) * NSEG, gp->local_pixels * frames);
@@ -1490,7 +1564,8 @@ int capacity_for(int frames) {
 size_t pass_bytes(int frames, bool staged) {
     const size_t cap = (size_t)capacity_for(frames);
     size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
-    if (gp->split) b += 4 * sizeof(float4) * (size_t)gp->local_pixels * frames;       // traversal queue
+    if (gp->split)   // traversal queue
+        b += (PT_QIDX ? sizeof(float4) + sizeof(int2) : 4 * sizeof(float4)) * (size_t)q_stride_for(frames) * NSEG;
     if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
     if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
     return b;
@@ -1511,11 +1586,16 @@ int ensure_frames(int frames) {
     gp->capacity = capacity_for(frames);
     for (int i = 0; i < 2; ++i)
         for (int k = 0; k < 3; ++k) RC(dalloc(&gp->d_path[i][k], (size_t)gp->capacity));
-    if (gp->split) {
-        const size_t qn = (size_t)gp->local_pixels * frames;
-        RC(dalloc(&gp->queue.A, qn));
-        RC(dalloc(&gp->queue.B, qn));
-        RC(dalloc(&gp->queue.C, qn));
+    if (gp->split) {   // NSEG queue segments, each room for the queued rays of its k_bounce blocks
+        gp->queue.stride = q_stride_for(frames);
+        const size_t qn = (size_t)gp->queue.stride * NSEG;
+        if (PT_QIDX) {
+            RC(dalloc(&gp->queue.E, qn));
+        } else {
+            RC(dalloc(&gp->queue.A, qn));
+            RC(dalloc(&gp->queue.B, qn));
+            RC(dalloc(&gp->queue.C, qn));
+        }
         RC(dalloc(&gp->queue.D, qn));
     }
     if (frames > 1) RC(dalloc(&gp->d_contrib, (size_t)gp->pixels_total * 3 * frames));
@@ -2922,7 +3002,9 @@ static int32_t frame_stats(pt_frame_stats* out) {
         int64_t cur = 0;
         for (int k = 0; k < NSEG; ++k) cur += ctl.cnt[b][k][0];
         out->live_total[b] = (int64_t)ctl.tot[b] + (ctl.frames > 0 ? cur : 0);
-        out->queued_total[b] = (int64_t)ctl.qtot[b] + (ctl.frames > 0 ? ctl.qcnt[b][0] : 0);
+        int64_t q = 0;
+        for (int k = 0; k < NSEG; ++k) q += ctl.qcnt[b][k][0];
+        out->queued_total[b] = (int64_t)ctl.qtot[b] + (ctl.frames > 0 ? q : 0);
         if (b < out->bounces) out->segments_total += out->live_total[b];
     }
     return PT_OK;

@@ -28,6 +28,12 @@ for s in "$@"; do
         benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
         multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
         inproc) step inproc 200 python bench.py --gpus 2 --inproc --inproc-devices 0,0 --steps 20 --warmup 5 ;;
+        ab_*)   # ab_<tag>: AB_LIBS / AB_ROUNDS from the environment, scenes below
+            tag=${s#ab_}
+            B=project3-cuda-path-tracer-2025_amd/build/ab
+            AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
+            AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
+            AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
