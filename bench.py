@@ -439,8 +439,18 @@ def api_frame_ms(tr, first_iteration, frames=40, warm=5):
         return round(ts[len(ts) // 2], 4), round(ts[int(0.9 * (len(ts) - 1))], 4)
     m_copy, p_copy = run(True, first_iteration)
     m_nc, p_nc = run(False, first_iteration + warm + frames)
+    # the same calls with the next-frame speculation off (PT_SPECULATE=0, read per call): every
+    # frame traced inside its own call, strictly before its copy
+    os.environ["PT_SPECULATE"] = "0"
+    try:
+        m_ns, p_ns = run(True, first_iteration + 2 * (warm + frames))
+    finally:
+        del os.environ["PT_SPECULATE"]
     return {"ms_per_frame": m_copy, "p90": p_copy, "ms_per_frame_no_copy": m_nc, "p90_no_copy": p_nc,
-            "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into the caller's pageable host memory per call"}
+            "ms_per_frame_no_speculation": m_ns, "p90_no_speculation": p_ns,
+            "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into the caller's pageable host memory per call; "
+                                      "frame N+1 is traced on a second stream while frame N's image is copied "
+                                      "(taken over bit-exactly by the call for N+1)"}
 
 
 def _device_tensor(torch, ptr, n, device):

@@ -100,7 +100,8 @@ constexpr int GRID_MIN_GEOMS = 16;
 struct FrameCtl {
     int iter;           // iteration of the pass's first frame (slot s traces iter + s)
     int batch;          // frames in the current pass
-    int _pad[2];
+    int plane;          // 1: a single-frame pass stores its contributions to plane 0 (speculative frame)
+    int _pad;
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     unsigned long long qtot[MAXB + 1];      // the same for qcnt (paths of bounce b queued for traversal)

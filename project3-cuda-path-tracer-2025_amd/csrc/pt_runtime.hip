@@ -46,7 +46,7 @@ using namespace ptd;
 // iteration, zero the per-pass counters and start a pass of `batch` frames.  One block.
 // `rows`: the counter rows any pass since the last reset of the block wrote (trace depth + 1 at
 // most; the rest stay zero), so a frame clears 9 rows of 8 segments at depth 8, not 65.
-__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int batch, int rows) {
+__global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int batch, int rows, int plane) {
     int t = threadIdx.x;
     if (ctl->frames > 0) {
         for (int b = t; b < rows; b += blockDim.x) {
@@ -65,6 +65,7 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
         ctl->batch = batch;
+        ctl->plane = plane;
         ctl->cnt[0][0][0] = local_pixels * batch;
         ctl->frames += batch;
     }
@@ -82,8 +83,8 @@ PT_DEV int mbcnt(uint64_t m) {
 // path's colour once).  Single-frame pass: add it now.  Pass of F > 1 frames: store it in the
 // frame's contribution plane; k_combine adds the planes in frame order afterwards, so the
 // image sees the same float additions in the same order as F sequential frames.
-PT_DEV void gather_into_image(float* image, const SceneDev& sc, int batch, const PathReg& p) {
-    if (batch > 1) {
+PT_DEV void gather_into_image(float* image, const SceneDev& sc, bool to_plane, const PathReg& p) {
+    if (to_plane) {
         float* px = sc.contrib + 3 * ((size_t)p.slot * (size_t)(sc.cam.resx * sc.cam.resy) + (size_t)p.pix);
         px[0] = p.c.x;
         px[1] = p.c.y;
@@ -115,6 +116,50 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
     px[0] = r;
     px[1] = gch;
     px[2] = b;
+}
+
+// A speculative single frame (spec_*) taken over by the call that asks for it: image += its plane
+// (the same float additions, in the same order, as its paths' gathers into the image would have
+// made) ...
+__global__ __launch_bounds__(BLOCK) void k_add_plane(SceneDev sc, const float* __restrict__ plane,
+                                                     float* __restrict__ image) {
+    const int l = blockIdx.x * BLOCK + threadIdx.x;
+    if (l >= sc.shard.local_pixels) return;
+    const size_t pix = 3 * (size_t)shard_pixel(sc, l);
+    float* px = image + pix;
+    const float* c = plane + pix;
+    const float r = px[0] + c[0], g = px[1] + c[1], b = px[2] + c[2];
+    px[0] = r;
+    px[1] = g;
+    px[2] = b;
+}
+// ... and the caller's FrameCtl takes its counters: the previous frame folded into the running
+// totals and the speculative frame's live counts in its place, as k_frame_begin and that frame's
+// kernels would have left them.  One block.
+__global__ void k_adopt_frame(FrameCtl* ctl, const FrameCtl* spec, int rows) {
+    const int t = threadIdx.x;
+    if (ctl->frames > 0) {
+        for (int b = t; b < rows; b += blockDim.x) {
+            unsigned long long s = 0, q = 0;
+            for (int k = 0; k < NSEG; ++k) {
+                s += (unsigned)ctl->cnt[b][k][0];
+                q += (unsigned)ctl->qcnt[b][k][0];
+            }
+            ctl->tot[b] += s;
+            ctl->qtot[b] += q;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < rows * NSEG; i += blockDim.x) {
+        (&ctl->cnt[0][0][0])[i * CNT_PAD] = (&spec->cnt[0][0][0])[i * CNT_PAD];
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD] = (&spec->qcnt[0][0][0])[i * CNT_PAD];
+    }
+    if (t == 0) {
+        ctl->iter = spec->iter;
+        ctl->batch = 1;
+        ctl->plane = 0;
+        ctl->frames += 1;
+    }
 }
 
 // Multi-device combine (pt_options.num_devices > 1): shard k owns the pixels
@@ -263,7 +308,7 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
     //              [VAR_WAVE_REDIST: one WaveLds per wave]
     extern __shared__ float4 s_dyn[];
     const int iter = ctl->iter;
-    const int batch = ctl->batch;
+    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     int n;
     int segoff[NSEG + 1];
     if (FIRST) {
@@ -372,7 +417,7 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
     }
     if (TIMING && active) tc = sec_clock();
     const bool surv = active && !queued && p.rb > 0;
-    if (active && !queued && !surv) gather_into_image(image, sc, batch, p);
+    if (active && !queued && !surv) gather_into_image(image, sc, to_plane, p);
     const int lane = tid & 63;
     const int seg = blockIdx.x & (NSEG - 1);
     if (VAR & VAR_WAVE_ATOMIC) {
@@ -419,7 +464,7 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
     extern __shared__ float4 s_dyn[];
     __shared__ int s_cnt[BLOCK / 64];
     const int iter = ctl->iter;
-    const int batch = ctl->batch;
+    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     int segoff[NSEG + 1];
     segoff[0] = 0;
 #pragma unroll
@@ -454,7 +499,7 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
         if (live) {
             const Hit h = finish_hit<false>(sc, p.o, p.d, nullptr, qt, qw, qs);
             shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
-            if (p.rb <= 0) gather_into_image(image, sc, batch, p);
+            if (p.rb <= 0) gather_into_image(image, sc, to_plane, p);
         }
         // paths entering bounce b + 1 (k_bounce's survivor count for this bounce)
         const bool surv = live && p.rb > 0;
@@ -497,7 +542,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     if (block_start >= n) return;
     int* s_stack = reinterpret_cast<int*>(s_dyn);
     const int iter = ctl->iter;
-    const int batch = ctl->batch;
+    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     const int tid = threadIdx.x;
     const int gid = block_start + tid;
     const bool active = gid < n;
@@ -562,7 +607,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
         shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
     const bool surv = active && p.rb > 0;
-    if (active && !surv) gather_into_image(image, sc, batch, p);
+    if (active && !surv) gather_into_image(image, sc, to_plane, p);
     const int seg = blockIdx.x & (NSEG - 1);
     int si, unused;
     block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
@@ -641,7 +686,8 @@ __global__ __launch_bounds__(BLOCK) void k_shade(SceneDev sc, PathBuf buf, HitBu
         return a;
     });
     store_path(buf, i, p);
-    if (p.rb <= 0 && image) gather_into_image(image, sc, iter_override > 0 ? 1 : ctl->batch, p);
+    if (p.rb <= 0 && image)
+        gather_into_image(image, sc, iter_override > 0 ? false : (ctl->batch > 1 || ctl->plane != 0), p);
     if (alive) alive[i] = p.rb > 0;
 }
 
@@ -1002,6 +1048,14 @@ struct State {
     int frames_done = 0;
     int32_t* traced_depth = nullptr;
     int* h_cnt = nullptr;            // page-locked copy of the live counters (TracedDepth, frame_depth_*)
+    // single-frame speculation (pt_trace, spec_*): frame N + 1 traced into a plane of its own on a
+    // second stream while frame N's image crosses PCIe to the caller
+    hipStream_t spec_stream = nullptr;
+    hipEvent_t spec_ev_in = nullptr;      // gp->stream: what the speculative frame follows
+    hipEvent_t spec_ev_done = nullptr;    // spec_stream: the speculative frame is finished
+    FrameCtl* d_ctl_spec = nullptr;       // its own counters (d_ctl keeps the caller's frame)
+    float* d_spec_plane = nullptr;        // its contributions, one float3 per pixel
+    int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
     int key_bits = 1;
 };
 State g_primary;                 // the process's context (shard 0 of a multi-device context)
@@ -1292,9 +1346,9 @@ int enqueue_pass_body(int batch) {
     return PT_OK;
 }
 
-int enqueue_pass(int set_iter, int batch) {
+int enqueue_pass(int set_iter, int batch, int plane = 0) {
     gp->ctl_rows = std::max(gp->ctl_rows, std::min(MAXB + 1, gp->sc.trace_depth + 1));
-    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, gp->d_ctl, set_iter, gp->local_pixels, batch, gp->ctl_rows);
+    launch(-1, k_frame_begin, dim3(1), dim3(256), 0, gp->d_ctl, set_iter, gp->local_pixels, batch, gp->ctl_rows, plane);
     HIPCHK(hipGetLastError());
     RC(enqueue_pass_body(batch));
     if (batch > 1) {
@@ -1340,6 +1394,82 @@ int run_pass(int iter, int batch) {
     return PT_OK;
 }
 int run_frame(int iter) { return run_pass(iter, 1); }
+
+// ---- single-frame speculation -----------------------------------------------------------------
+// main.cpp calls pathtrace(pbo, frame, ++iteration) every frame and copies the 7.68 MB image to
+// pageable host memory each time (pathtrace.cu:783): on MI355X that copy (~0.15 ms over PCIe) is
+// longer than the frame's kernels (~0.12 ms).  So once frame N is traced, frame N + 1 is traced
+// at once on a second stream -- into a plane of its own with a FrameCtl of its own, the accumulated
+// image untouched -- while frame N's image is copied out.  The call for iteration N + 1 then only
+// adds that plane to the image (k_add_plane: the same additions as the frame's own gathers) and
+// takes over its counters (k_adopt_frame), bit for bit what tracing it then would have produced.
+// Any call that could make it differ (another iteration, a camera or depth change, multi-frame
+// passes, the test and profiling entry points) first waits for it and drops it (spec_cancel).
+// PT_SPECULATE=0 turns it off.  One device context, fused pipeline.
+bool spec_enabled() {
+    const char* e = getenv("PT_SPECULATE");   // read per call: tests and bench.py compare both
+    return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED;
+}
+int spec_cancel() {
+    if (gp->spec_iter == 0) return PT_OK;
+    gp->spec_iter = 0;
+    HIPCHK(hipStreamSynchronize(gp->spec_stream));
+    return PT_OK;
+}
+void spec_release() {
+    if (gp->spec_stream) (void)hipStreamSynchronize(gp->spec_stream);
+    if (gp->spec_ev_in) (void)hipEventDestroy(gp->spec_ev_in);
+    if (gp->spec_ev_done) (void)hipEventDestroy(gp->spec_ev_done);
+    if (gp->spec_stream) (void)hipStreamDestroy(gp->spec_stream);
+    if (gp->d_ctl_spec) (void)hipFree(gp->d_ctl_spec);
+    if (gp->d_spec_plane) (void)hipFree(gp->d_spec_plane);
+    gp->spec_stream = nullptr;
+    gp->spec_ev_in = gp->spec_ev_done = nullptr;
+    gp->d_ctl_spec = nullptr;
+    gp->d_spec_plane = nullptr;
+    gp->spec_iter = 0;
+}
+// queue frame `iter` on the speculation stream, behind everything queued on gp->stream so far
+int spec_launch(int iter) {
+    if (!gp->spec_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&gp->spec_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&gp->spec_ev_in, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&gp->spec_ev_done, hipEventDisableTiming));
+        HIPCHK(hipMalloc((void**)&gp->d_ctl_spec, sizeof(FrameCtl)));
+        HIPCHK(hipMemsetAsync(gp->d_ctl_spec, 0, sizeof(FrameCtl), gp->spec_stream));
+        HIPCHK(hipMalloc((void**)&gp->d_spec_plane, sizeof(float) * 3 * (size_t)gp->pixels_total));
+    }
+    HIPCHK(hipEventRecord(gp->spec_ev_in, gp->stream));
+    HIPCHK(hipStreamWaitEvent(gp->spec_stream, gp->spec_ev_in, 0));
+    hipStream_t main_stream = gp->stream;
+    FrameCtl* main_ctl = gp->d_ctl;
+    float* main_contrib = gp->sc.contrib;
+    gp->stream = gp->spec_stream;
+    gp->d_ctl = gp->d_ctl_spec;
+    gp->sc.contrib = gp->d_spec_plane;
+    const int rc = enqueue_pass(iter, 1, 1);
+    gp->stream = main_stream;
+    gp->d_ctl = main_ctl;
+    gp->sc.contrib = main_contrib;
+    RC(rc);
+    HIPCHK(hipEventRecord(gp->spec_ev_done, gp->spec_stream));
+    gp->spec_iter = iter;
+    return PT_OK;
+}
+// the call for the speculative frame's iteration: take it over on gp->stream
+int spec_adopt() {
+    const int iter = gp->spec_iter;
+    HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
+    launch(7, k_add_plane, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane,
+           gp->d_image);
+    launch(7, k_adopt_frame, dim3(1), dim3(256), 0, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
+    HIPCHK(hipGetLastError());
+    gp->spec_iter = 0;
+    gp->dev_iter = iter;
+    gp->last_iter = iter;
+    gp->frames_done += 1;
+    return PT_OK;
+}
 
 // frames of the next pass when `remaining` frames are left: the passes of a run are balanced
 // (100 frames at F = 32 -> 4 x 25, not 32 + 32 + 32 + 4: a small last pass runs its launches
@@ -1638,6 +1768,7 @@ int ensure_test_paths(int64_t n) {
 }
 
 void free_all() {
+    spec_release();
     release_graph();
     free_pass_buffers();
     void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
@@ -1812,7 +1943,8 @@ struct ShardScope {
 };
 
 int need_single(const char* what) {
-    return M.n > 1 ? fail(PT_E_UNSUPPORTED, "%s: one device context only (pt_options.num_devices > 1)", what) : PT_OK;
+    if (M.n > 1) return fail(PT_E_UNSUPPORTED, "%s: one device context only (pt_options.num_devices > 1)", what);
+    return spec_cancel();   // the test / profiling entry points use the path buffers themselves
 }
 
 void multi_release() {
@@ -2801,6 +2933,7 @@ int32_t pt_set_camera(const pt_camera* c) {
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (memcmp(&nc, &gp->sc.cam, sizeof nc) != 0) {
+            RC(spec_cancel());                          // traced with the old camera
             HIPCHK(hipStreamSynchronize(gp->stream));   // a replayed pass may still hold the graph
             gp->sc.cam = nc;
             release_graph();   // kernel arguments changed
@@ -2815,6 +2948,7 @@ int32_t pt_set_trace_depth(int32_t depth) {
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (gp->sc.trace_depth != depth) {
+            RC(spec_cancel());
             HIPCHK(hipStreamSynchronize(gp->stream));
             gp->sc.trace_depth = depth;
             release_graph();   // the bounce count is baked into the captured passes
@@ -2827,9 +2961,15 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     (void)frame;   // unused by the reference too (pathtrace.cu:639)
     RC(need_init());
     if (iteration <= 0) return fail(PT_E_INVALID, "iteration is 1-based (main.cpp:458), got %d", iteration);
+    const bool spec = M.n <= 1 && spec_enabled();
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
-        RC(run_frame(iteration));
+        if (spec && gp->spec_iter == iteration) {
+            RC(spec_adopt());          // traced already, during the previous call's image copy
+        } else {
+            RC(spec_cancel());
+            RC(run_frame(iteration));
+        }
         if (g_primary.traced_depth) RC(frame_depth_enqueue());   // read after the one sync below
     }
     RC(multi_combine());
@@ -2838,6 +2978,9 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
                            gp->pixels_total, iteration);
         HIPCHK(hipGetLastError());
     }
+    // the next frame, on the second stream, while this one's image is copied out (queued before
+    // the copy: a copy into pageable memory may hold the host until it is done)
+    if (spec && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
     if (host_image) {
         // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new
@@ -2864,6 +3007,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
 
 int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     RC(need_init());
+    RC(spec_cancel());
     if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
     // passes of gp->batch frames (bit-identical to frame-by-frame: k_combine keeps the order);
     // every shard's passes are queued before the combine, so the devices trace concurrently
@@ -2880,6 +3024,7 @@ int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
 
 int32_t pt_prepare_frames(int32_t count) {
     RC(need_init());
+    RC(spec_cancel());
     if (count < 0) return fail(PT_E_INVALID, "bad count");
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
@@ -2897,6 +3042,7 @@ int32_t pt_prepare_frames(int32_t count) {
 
 int32_t pt_synchronize(void) {
     RC(need_init());
+    if (g_primary.spec_stream) HIPCHK(hipStreamSynchronize(g_primary.spec_stream));   // it stays valid
     for (int k = nshards() - 1; k >= 0; --k) {
         ShardScope sc(shard_ctx(k));
         HIPCHK(hipStreamSynchronize(gp->stream));
@@ -3030,7 +3176,7 @@ int32_t pt_test_camera(int32_t iteration, pt_path_segment* out, int64_t n) {
     RC(ensure_frames(1));
     RC(ctl_reset());
     hipLaunchKernelGGL(k_frame_begin, dim3(1), dim3(256), 0, gp->stream, gp->d_ctl, iteration, gp->local_pixels, 1,
-                       gp->ctl_rows);
+                       gp->ctl_rows, 0);
     hipLaunchKernelGGL(k_camera, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->stream, gp->sc, pathbuf(0), gp->d_ctl);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(gp->stream));
