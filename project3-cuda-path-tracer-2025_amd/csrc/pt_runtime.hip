@@ -118,12 +118,40 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
     px[2] = b;
 }
 
-// A speculative single frame (spec_*) taken over by the call that asks for it: image += its plane
-// (the same float additions, in the same order, as its paths' gathers into the image would have
-// made) ...
-__global__ __launch_bounds__(BLOCK) void k_add_plane(SceneDev sc, const float* __restrict__ plane,
-                                                     float* __restrict__ image) {
-    const int l = blockIdx.x * BLOCK + threadIdx.x;
+// A speculative single frame (spec_*) taken over by the call that asks for it, in one launch:
+// image += its plane (the same float additions, in the same order, as its paths' gathers into the
+// image would have made), and block 0 gives the caller's FrameCtl its counters -- the previous
+// frame folded into the running totals and the speculative frame's live counts in its place, as
+// k_frame_begin and that frame's kernels would have left them.
+__global__ __launch_bounds__(BLOCK) void k_adopt_frame(SceneDev sc, const float* __restrict__ plane,
+                                                       float* __restrict__ image, FrameCtl* ctl,
+                                                       const FrameCtl* spec, int rows) {
+    const int t = threadIdx.x;
+    if (blockIdx.x == 0) {
+        if (ctl->frames > 0) {
+            for (int b = t; b < rows; b += BLOCK) {
+                unsigned long long s = 0, q = 0;
+                for (int k = 0; k < NSEG; ++k) {
+                    s += (unsigned)ctl->cnt[b][k][0];
+                    q += (unsigned)ctl->qcnt[b][k][0];
+                }
+                ctl->tot[b] += s;
+                ctl->qtot[b] += q;
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < rows * NSEG; i += BLOCK) {
+            (&ctl->cnt[0][0][0])[i * CNT_PAD] = (&spec->cnt[0][0][0])[i * CNT_PAD];
+            (&ctl->qcnt[0][0][0])[i * CNT_PAD] = (&spec->qcnt[0][0][0])[i * CNT_PAD];
+        }
+        if (t == 0) {
+            ctl->iter = spec->iter;
+            ctl->batch = 1;
+            ctl->plane = 0;
+            ctl->frames += 1;
+        }
+    }
+    const int l = blockIdx.x * BLOCK + t;
     if (l >= sc.shard.local_pixels) return;
     const size_t pix = 3 * (size_t)shard_pixel(sc, l);
     float* px = image + pix;
@@ -132,34 +160,6 @@ __global__ __launch_bounds__(BLOCK) void k_add_plane(SceneDev sc, const float* _
     px[0] = r;
     px[1] = g;
     px[2] = b;
-}
-// ... and the caller's FrameCtl takes its counters: the previous frame folded into the running
-// totals and the speculative frame's live counts in its place, as k_frame_begin and that frame's
-// kernels would have left them.  One block.
-__global__ void k_adopt_frame(FrameCtl* ctl, const FrameCtl* spec, int rows) {
-    const int t = threadIdx.x;
-    if (ctl->frames > 0) {
-        for (int b = t; b < rows; b += blockDim.x) {
-            unsigned long long s = 0, q = 0;
-            for (int k = 0; k < NSEG; ++k) {
-                s += (unsigned)ctl->cnt[b][k][0];
-                q += (unsigned)ctl->qcnt[b][k][0];
-            }
-            ctl->tot[b] += s;
-            ctl->qtot[b] += q;
-        }
-    }
-    __syncthreads();
-    for (int i = t; i < rows * NSEG; i += blockDim.x) {
-        (&ctl->cnt[0][0][0])[i * CNT_PAD] = (&spec->cnt[0][0][0])[i * CNT_PAD];
-        (&ctl->qcnt[0][0][0])[i * CNT_PAD] = (&spec->qcnt[0][0][0])[i * CNT_PAD];
-    }
-    if (t == 0) {
-        ctl->iter = spec->iter;
-        ctl->batch = 1;
-        ctl->plane = 0;
-        ctl->frames += 1;
-    }
 }
 
 // Multi-device combine (pt_options.num_devices > 1): shard k owns the pixels
@@ -1018,6 +1018,7 @@ struct State {
     DevPair* d_pairs = nullptr;
     DevTriHot* d_hot4 = nullptr;
     float4* d_leaf9 = nullptr;
+    uint4* d_pq = nullptr;           // PT_BVH_Q16 inner records
     DevTriCold* d_cold = nullptr;
     float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     float4* d_hit_nt = nullptr;
@@ -1405,7 +1406,8 @@ int run_frame(int iter) { return run_pass(iter, 1); }
 // takes over its counters (k_adopt_frame), bit for bit what tracing it then would have produced.
 // Any call that could make it differ (another iteration, a camera or depth change, multi-frame
 // passes, the test and profiling entry points) first waits for it and drops it (spec_cancel).
-// PT_SPECULATE=0 turns it off.  One device context, fused pipeline.
+// Only calls that copy the image out start one.  PT_SPECULATE=0 turns it off.  One device
+// context, fused pipeline.
 bool spec_enabled() {
     const char* e = getenv("PT_SPECULATE");   // read per call: tests and bench.py compare both
     return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED;
@@ -1460,9 +1462,8 @@ int spec_launch(int iter) {
 int spec_adopt() {
     const int iter = gp->spec_iter;
     HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
-    launch(7, k_add_plane, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane,
-           gp->d_image);
-    launch(7, k_adopt_frame, dim3(1), dim3(256), 0, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
+    launch(7, k_adopt_frame, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane,
+           gp->d_image, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
     HIPCHK(hipGetLastError());
     gp->spec_iter = 0;
     gp->dev_iter = iter;
@@ -1772,7 +1773,8 @@ void free_all() {
     release_graph();
     free_pass_buffers();
     void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
-                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid};
+                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid,
+                    gp->d_pq};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (gp->stream) (void)hipStreamDestroy(gp->stream);
@@ -2397,6 +2399,8 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<DevTriHot> hot;
     std::vector<DevTriCold> cold;
     std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
+    std::vector<uint4> pq;           // PT_BVH_Q16 inner records
+    float q16_lo[3] = {0.f, 0.f, 0.f}, q16_cell[3] = {0.f, 0.f, 0.f}, q16_2_over_E = 0.f;
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0;
@@ -2713,6 +2717,68 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;
+#if PT_BVH_Q16
+                {   // pair_q16 records (pt_kernels.h PT_BVH_Q16): the grid is the root box grown by
+                    // m on every side, 65535 cells per axis, in the floats the device will use
+                    const double m = 2e-5 * cull_extent;
+                    const float rl[3] = {nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z};
+                    const float rh[3] = {nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z};
+                    for (int a = 0; a < 3; ++a) {
+                        float g = (float)((double)rl[a] - m);
+                        if ((double)g > (double)rl[a] - m) g = std::nextafter(g, -HUGE_VALF);
+                        float c = (float)(((double)rh[a] + m - (double)g) / 65535.0);
+                        if ((double)g + 65535.0 * (double)c < (double)rh[a] + m) c = std::nextafter(c, HUGE_VALF);
+                        q16_lo[a] = g;
+                        q16_cell[a] = c;
+                    }
+                    auto quant = [&](float v, int a, bool up) -> uint32_t {
+                        const double x = ((double)v + (up ? m : -m) - (double)q16_lo[a]) / (double)q16_cell[a];
+                        const double q = up ? std::ceil(x) : std::floor(x);
+                        return (uint32_t)std::min(65535.0, std::max(0.0, q));
+                    };
+                    pq.assign(2 * (size_t)P, make_uint4(0, 0, 0, 0));
+                    for (int i = 0; i < P; ++i) {
+                        const DevPair& pr = pairs[i];
+                        const float4* lo[2] = {&pr.l_lo, &pr.r_lo};
+                        const float4* hi[2] = {&pr.l_hi, &pr.r_hi};
+                        uint32_t q[2][6], ref[2], A[2];
+                        for (int k = 0; k < 2; ++k) {
+                            const float l3[3] = {lo[k]->x, lo[k]->y, lo[k]->z}, h3[3] = {hi[k]->x, hi[k]->y, hi[k]->z};
+                            for (int a = 0; a < 3; ++a) {
+                                q[k][a] = quant(l3[a], a, false);
+                                q[k][3 + a] = quant(h3[a], a, true);
+                            }
+                            int rf;
+                            memcpy(&rf, &lo[k]->w, 4);
+                            ref[k] = (uint32_t)rf;
+                            uint32_t w;
+                            memcpy(&w, &hi[k]->w, 4);
+                            A[k] = w >> 16;   // pack_cull's A, already rounded up to 16 bits
+                        }
+                        uint4& x = pq[2 * (size_t)i];
+                        uint4& y = pq[2 * (size_t)i + 1];
+                        x.x = q[0][0] | q[0][1] << 16;
+                        x.y = q[0][2] | q[0][3] << 16;
+                        x.z = q[0][4] | q[0][5] << 16;
+                        x.w = q[1][0] | q[1][1] << 16;
+                        y.x = q[1][2] | q[1][3] << 16;
+                        y.y = q[1][4] | q[1][5] << 16;
+                        y.z = ref[0] | ref[1] << 16;
+                        y.w = A[1] | A[0] << 16;
+                    }
+                    // leaves: the reference's exact box, then the 9 triangle float4
+                    std::vector<float4> l11(11 * (size_t)L);
+                    for (int k = 0; k < L; ++k) {
+                        const DevNode& nd = nodes[leaf_nodes[k]];
+                        l11[11 * (size_t)k] = make_float4(nd.lo.x, nd.lo.y, nd.lo.z, 0.f);
+                        l11[11 * (size_t)k + 1] = make_float4(nd.hi.x, nd.hi.y, nd.hi.z, 0.f);
+                        for (int j = 0; j < 9; ++j) l11[11 * (size_t)k + 2 + j] = leaf9[9 * (size_t)k + j];
+                    }
+                    leaf9.swap(l11);
+                    q16_2_over_E = (float)(2.0 / (double)Ef);
+                    if ((double)q16_2_over_E < 2.0 / (double)Ef) q16_2_over_E = std::nextafter(q16_2_over_E, HUGE_VALF);
+                }
+#endif
             }
         }
         gp->bvh_lds = (size_t)gp->stack_depth * BLOCK * sizeof(int);
@@ -2792,6 +2858,10 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
             RC(upload(gp->d_hot4, hot4.data(), hot4.size()));
             RC(dalloc(&gp->d_leaf9, leaf9.size()));
             RC(upload(gp->d_leaf9, leaf9.data(), leaf9.size()));
+            if (!pq.empty()) {
+                RC(dalloc(&gp->d_pq, pq.size()));
+                RC(upload(gp->d_pq, pq.data(), pq.size()));
+            }
         }
     }
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
@@ -2852,6 +2922,12 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.pairs = gp->d_pairs;
     sc.hot4 = gp->d_hot4;
     sc.leaf9 = gp->d_leaf9;
+    sc.pq = gp->d_pq;
+    for (int a = 0; a < 3; ++a) {
+        sc.q_lo[a] = q16_lo[a];
+        sc.q_cell[a] = q16_cell[a];
+    }
+    sc.cull_2_over_E = q16_2_over_E;
     sc.num_pairs = pair_count;
     sc.root_ref = pair_root_ref;
     sc.root_lo = pair_root_lo;
@@ -2961,7 +3037,9 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     (void)frame;   // unused by the reference too (pathtrace.cu:639)
     RC(need_init());
     if (iteration <= 0) return fail(PT_E_INVALID, "iteration is 1-based (main.cpp:458), got %d", iteration);
-    const bool spec = M.n <= 1 && spec_enabled();
+    // speculate only for callers that copy the image out (main.cpp's pathtrace() always does): a
+    // call without the copy has nothing for the next frame to overlap with
+    const bool spec = M.n <= 1 && spec_enabled() && (host_image != nullptr || gp->spec_iter == iteration);
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (spec && gp->spec_iter == iteration) {
@@ -2980,7 +3058,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     }
     // the next frame, on the second stream, while this one's image is copied out (queued before
     // the copy: a copy into pageable memory may hold the host until it is done)
-    if (spec && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
+    if (spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
     if (host_image) {
         // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new

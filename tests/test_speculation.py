@@ -82,7 +82,8 @@ def test_speculated_api_frames_bitexact(name, res, opts, oracle, ptamd, monkeypa
 
 
 def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
-    """the same call sequence with PT_SPECULATE=0 and with speculation: images and PBOs equal"""
+    """the same call sequence with PT_SPECULATE=0 and with speculation: images and PBOs equal;
+    a call without the host copy in the middle takes over the frame the previous one started"""
     a, b = _pair(oracle, ptamd, "cornell_glass_test", (48, 48))
     pbo = ctypes.c_void_p()
     assert ptamd.lib.pt_device_alloc(4 * a.pixelcount, ctypes.byref(pbo)) == 0
@@ -92,8 +93,9 @@ def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
             monkeypatch.setenv("PT_SPECULATE", mode)
             tr = ptamd.PathTracer(b)
             imgs, pbos = [], []
-            for it in (1, 2, 3, 5, 6):
-                imgs.append(tr.trace(it, pbo_device_ptr=pbo.value, copy_image=True).copy())
+            for it in (1, 2, 3, 5, 6, 7, 8):
+                tr.trace(it, pbo_device_ptr=pbo.value, copy_image=it != 6)
+                imgs.append(tr.image())
                 h = np.zeros((a.pixelcount, 4), np.uint8)
                 assert ptamd.lib.pt_device_read(h.ctypes.data, pbo, h.nbytes) == 0
                 pbos.append(h)
@@ -107,21 +109,21 @@ def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
 
 def test_camera_change_drops_the_speculated_frame(oracle, ptamd, monkeypatch):
     """pt_set_camera with a different camera between frames: the frame traced after it uses the
-    new camera (equal to a fresh tracer on the moved camera); setting the SAME camera keeps it"""
+    new camera (equal to a fresh tracer on the moved camera); setting the SAME camera keeps it.
+    (Speculation starts only in calls that copy the image out, as main.cpp's do.)"""
     monkeypatch.delenv("PT_SPECULATE", raising=False)
     a, b = _pair(oracle, ptamd, "cornell", (48, 48))
     b2 = ptamd.SceneFile(scene_path("cornell"), res=(48, 48))
     cam = b2.camera.copy()
     cam["position"][0][1] += 0.25                 # eye moved up
     tr = ptamd.PathTracer(b)
-    tr.trace(1)
-    tr.trace(2)
+    tr.trace(1, copy_image=True)
+    tr.trace(2, copy_image=True)
     assert ptamd.lib.pt_set_camera(b.camera.ctypes.data) == 0      # unchanged
-    tr.trace(3)
-    base = tr.image().copy()
+    base = tr.trace(3, copy_image=True).copy()
     assert ptamd.lib.pt_set_camera(cam.ctypes.data) == 0           # moved: frame 4 on the new camera
-    tr.trace(4)
-    got = tr.image()
+    got = tr.trace(4, copy_image=True).copy()
+    assert _eq(tr.image(), got)
     tr.free()
     # reference: frames 1..3 on the old camera, then frame 4 on the moved one, no speculation
     monkeypatch.setenv("PT_SPECULATE", "0")

@@ -20,7 +20,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(use_graph=1):
+def run(use_graph=1, copy=False):
     sys.path.insert(0, os.path.join(REPO, "project3-cuda-path-tracer-2025_amd"))
     import ptamd
     sc = ptamd.SceneFile(os.path.join(REPO, "scenes", "cornell.json"))
@@ -28,12 +28,47 @@ def run(use_graph=1):
     ts = []
     for k in range(100):
         t0 = time.perf_counter()
-        tr.trace(k + 1)
-        tr.synchronize()
+        tr.trace(k + 1, copy_image=copy)
+        if not copy:
+            tr.synchronize()
         if k >= 40:
             ts.append(1e3 * (time.perf_counter() - t0))
-    print(json.dumps({"wall_ms_per_call_median": round(st.median(ts), 4), "calls": len(ts), "use_graph": use_graph}))
+    print(json.dumps({"wall_ms_per_call_median": round(st.median(ts), 4), "calls": len(ts), "use_graph": use_graph,
+                      "host_copy": copy}))
     tr.free()
+
+
+def overlap(kernel_csv, copy_csv, out=None):
+    """`run copy` (main.cpp's call: image copied to the host every call) with --memory-copy-trace:
+    per device-to-host image copy, its duration and the share of it during which a kernel of the
+    next (speculated) frame was running -- the overlap pt_trace's speculation buys."""
+    kern = []
+    with open(kernel_csv) as f:
+        for r in csv.DictReader(f):
+            kern.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    kern.sort()
+    copies = []
+    with open(copy_csv) as f:
+        for r in csv.DictReader(f):
+            if "DEVICE_TO_HOST" in r.get("Direction", "") or "D2H" in r.get("Direction", ""):
+                copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    copies.sort()
+    copies = copies[-60:]
+    durs, shares = [], []
+    for s, e in copies:
+        busy = 0
+        for ks, ke in kern:
+            if ke <= s or ks >= e:
+                continue
+            busy += min(e, ke) - max(s, ks)
+        durs.append((e - s) / 1e3)
+        shares.append(min(1.0, busy / max(1, e - s)))
+    res = {"copies": len(copies), "copy_us_median": round(st.median(durs), 2) if durs else None,
+           "kernel_busy_share_during_copy_median": round(st.median(shares), 3) if shares else None}
+    print(json.dumps(res, indent=1))
+    if out:
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
 
 
 def analyse(path, out=None):
@@ -71,6 +106,8 @@ def analyse(path, out=None):
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run(0 if "eager" in sys.argv[2:] else 1)
+        run(0 if "eager" in sys.argv[2:] else 1, "copy" in sys.argv[2:])
+    elif sys.argv[1] == "overlap":
+        overlap(sys.argv[2], sys.argv[3], sys.argv[5] if len(sys.argv) > 5 and sys.argv[4] == "--out" else None)
     else:
         analyse(sys.argv[2], sys.argv[4] if len(sys.argv) > 4 and sys.argv[3] == "--out" else None)

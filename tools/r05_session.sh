@@ -22,6 +22,7 @@ for s in "$@"; do
         new) step pytest_new 500 $PYT tests/test_multi_device.py tests/test_dropin.py -m gpu ;;
         spec) step pytest_spec 300 $PYT tests/test_speculation.py -m gpu ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
+        meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
         mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
         gpu) step pytest_gpu 900 $PYT tests -m gpu ;;
         smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -32,7 +33,7 @@ for s in "$@"; do
         ab_*)   # ab_<tag>: AB_LIBS / AB_ROUNDS from the environment, scenes below
             tag=${s#ab_}
             B=project3-cuda-path-tracer-2025_amd/build/ab
-            AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
+            [ -z "${AB_SKIP_CORNELL:-}" ] && AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
             AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
             AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
