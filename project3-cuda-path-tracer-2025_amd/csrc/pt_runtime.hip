@@ -127,29 +127,39 @@ __global__ __launch_bounds__(BLOCK) void k_adopt_frame(SceneDev sc, const float*
                                                        float* __restrict__ image, FrameCtl* ctl,
                                                        const FrameCtl* spec, int rows) {
     const int t = threadIdx.x;
-    if (blockIdx.x == 0) {
-        if (ctl->frames > 0) {
-            for (int b = t; b < rows; b += BLOCK) {
-                unsigned long long s = 0, q = 0;
-                for (int k = 0; k < NSEG; ++k) {
-                    s += (unsigned)ctl->cnt[b][k][0];
-                    q += (unsigned)ctl->qcnt[b][k][0];
-                }
-                ctl->tot[b] += s;
-                ctl->qtot[b] += q;
-            }
-        }
-        __syncthreads();
-        for (int i = t; i < rows * NSEG; i += BLOCK) {
-            (&ctl->cnt[0][0][0])[i * CNT_PAD] = (&spec->cnt[0][0][0])[i * CNT_PAD];
-            (&ctl->qcnt[0][0][0])[i * CNT_PAD] = (&spec->qcnt[0][0][0])[i * CNT_PAD];
-        }
+    if (blockIdx.x == 0 && t < rows * NSEG) {   // one thread per (bounce row, segment), all loads at once
+        const bool fold = ctl->frames > 0;        // (frames only grows: a late reader folds the same zeros)
+        int* c = &ctl->cnt[0][0][0] + t * CNT_PAD;
+        int* q = &ctl->qcnt[0][0][0] + t * CNT_PAD;
+        const int c0 = *c, q0 = *q;
+        const int c1 = (&spec->cnt[0][0][0])[t * CNT_PAD], q1 = (&spec->qcnt[0][0][0])[t * CNT_PAD];
+        const int b = t / NSEG;
+        if (fold && c0) atomicAdd(&ctl->tot[b], (unsigned long long)(unsigned)c0);
+        if (fold && q0) atomicAdd(&ctl->qtot[b], (unsigned long long)(unsigned)q0);
+        *c = c1;
+        *q = q1;
         if (t == 0) {
             ctl->iter = spec->iter;
             ctl->batch = 1;
             ctl->plane = 0;
             ctl->frames += 1;
         }
+    }
+    if (sc.shard.mode != PT_SHARD_PIXELS) {   // every pixel: the planes as one float4 stream
+        const int nf = 3 * sc.shard.local_pixels;
+        const int i = 4 * (blockIdx.x * BLOCK + t);
+        if (i + 3 < nf) {
+            float4 x = *reinterpret_cast<const float4*>(image + i);
+            const float4 c = *reinterpret_cast<const float4*>(plane + i);
+            x.x += c.x;
+            x.y += c.y;
+            x.z += c.z;
+            x.w += c.w;
+            *reinterpret_cast<float4*>(image + i) = x;
+        } else {
+            for (int k = i; k < nf; ++k) image[k] += plane[k];
+        }
+        return;
     }
     const int l = blockIdx.x * BLOCK + t;
     if (l >= sc.shard.local_pixels) return;
@@ -1056,7 +1066,10 @@ struct State {
     hipEvent_t spec_ev_done = nullptr;    // spec_stream: the speculative frame is finished
     FrameCtl* d_ctl_spec = nullptr;       // its own counters (d_ctl keeps the caller's frame)
     float* d_spec_plane = nullptr;        // its contributions, one float3 per pixel
+    hipGraph_t spec_graph = nullptr;      // its pass, captured once (released with the pass graphs)
+    hipGraphExec_t spec_exec = nullptr;
     int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
+    int spec_dev_iter = 0;                // d_ctl_spec->iter after the speculative frames queued so far
     int key_bits = 1;
 };
 State g_primary;                 // the process's context (shard 0 of a multi-device context)
@@ -1128,6 +1141,10 @@ void launch(int kind, K kernel, dim3 grid, dim3 block, uint32_t lds, A... args) 
 int nblocks(int n) { return (n + BLOCK - 1) / BLOCK; }
 
 void release_graph() {
+    if (gp->spec_exec) (void)hipGraphExecDestroy(gp->spec_exec);
+    if (gp->spec_graph) (void)hipGraphDestroy(gp->spec_graph);
+    gp->spec_exec = nullptr;
+    gp->spec_graph = nullptr;
     for (int f = 0; f <= MAXF; ++f) {
         if (gp->graph_exec[f]) (void)hipGraphExecDestroy(gp->graph_exec[f]);
         if (gp->graph[f]) (void)hipGraphDestroy(gp->graph[f]);
@@ -1430,6 +1447,7 @@ void spec_release() {
     gp->d_ctl_spec = nullptr;
     gp->d_spec_plane = nullptr;
     gp->spec_iter = 0;
+    gp->spec_dev_iter = 0;
 }
 // queue frame `iter` on the speculation stream, behind everything queued on gp->stream so far
 int spec_launch(int iter) {
@@ -1441,19 +1459,35 @@ int spec_launch(int iter) {
         HIPCHK(hipMemsetAsync(gp->d_ctl_spec, 0, sizeof(FrameCtl), gp->spec_stream));
         HIPCHK(hipMalloc((void**)&gp->d_spec_plane, sizeof(float) * 3 * (size_t)gp->pixels_total));
     }
+    if (!gp->spec_exec) {   // captured once (released with the pass graphs: camera, depth, buffers)
+        hipStream_t main_stream = gp->stream;
+        FrameCtl* main_ctl = gp->d_ctl;
+        float* main_contrib = gp->sc.contrib;
+        gp->stream = gp->spec_stream;
+        gp->d_ctl = gp->d_ctl_spec;
+        gp->sc.contrib = gp->d_spec_plane;
+        hipError_t e = hipStreamBeginCapture(gp->spec_stream, hipStreamCaptureModeThreadLocal);
+        const int rc = e == hipSuccess ? enqueue_pass(0, 1, 1) : PT_OK;   // iteration: the device's + 1
+        hipGraph_t gr = nullptr;
+        if (e == hipSuccess) e = hipStreamEndCapture(gp->spec_stream, &gr);
+        gp->stream = main_stream;
+        gp->d_ctl = main_ctl;
+        gp->sc.contrib = main_contrib;
+        RC(rc);
+        HIPCHK(e);
+        gp->spec_graph = gr;
+        HIPCHK(hipGraphInstantiate(&gp->spec_exec, gr, nullptr, nullptr, 0));
+    }
+    // behind gp->stream's work so far; ONE graph launch, so that the image copy the caller queues
+    // next starts without waiting for the host to launch six kernels
     HIPCHK(hipEventRecord(gp->spec_ev_in, gp->stream));
     HIPCHK(hipStreamWaitEvent(gp->spec_stream, gp->spec_ev_in, 0));
-    hipStream_t main_stream = gp->stream;
-    FrameCtl* main_ctl = gp->d_ctl;
-    float* main_contrib = gp->sc.contrib;
-    gp->stream = gp->spec_stream;
-    gp->d_ctl = gp->d_ctl_spec;
-    gp->sc.contrib = gp->d_spec_plane;
-    const int rc = enqueue_pass(iter, 1, 1);
-    gp->stream = main_stream;
-    gp->d_ctl = main_ctl;
-    gp->sc.contrib = main_contrib;
-    RC(rc);
+    // the captured k_frame_begin advances the speculative FrameCtl's iteration by one: preset it
+    // only when the last speculative frame was not iter - 1 (consecutive calls launch the graph alone)
+    if (gp->spec_dev_iter != iter - 1)
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&gp->d_ctl_spec->iter, iter - 1, 1, gp->spec_stream));
+    HIPCHK(hipGraphLaunch(gp->spec_exec, gp->spec_stream));
+    gp->spec_dev_iter = iter;
     HIPCHK(hipEventRecord(gp->spec_ev_done, gp->spec_stream));
     gp->spec_iter = iter;
     return PT_OK;
@@ -1462,8 +1496,9 @@ int spec_launch(int iter) {
 int spec_adopt() {
     const int iter = gp->spec_iter;
     HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
-    launch(7, k_adopt_frame, dim3(nblocks(gp->local_pixels)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane,
-           gp->d_image, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
+    const int items = gp->sc.shard.mode != PT_SHARD_PIXELS ? (3 * gp->local_pixels + 3) / 4 : gp->local_pixels;
+    launch(7, k_adopt_frame, dim3(nblocks(items)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane, gp->d_image,
+           gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
     HIPCHK(hipGetLastError());
     gp->spec_iter = 0;
     gp->dev_iter = iter;
@@ -3058,7 +3093,14 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     }
     // the next frame, on the second stream, while this one's image is copied out (queued before
     // the copy: a copy into pageable memory may hold the host until it is done)
-    if (spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
+    static const bool copy_first = getenv("PT_SPEC_COPY_FIRST") && atoi(getenv("PT_SPEC_COPY_FIRST")) != 0;  // tools: A/B
+    if (!copy_first && spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
+    if (host_image && copy_first) {
+        const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
+        HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
+        if (spec && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
+        host_image = nullptr;
+    }
     if (host_image) {
         // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new

@@ -36,6 +36,19 @@ for s in "$@"; do
             [ -z "${AB_SKIP_CORNELL:-}" ] && AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
             AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
             AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
+        secq16)
+            PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/q16.so step sec_q16_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_q16_bunny.json
+            PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/q16.so step sec_q16_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_q16_khaslana.json ;;
+        profiles) step profiles 1100 bash tools/r05_profiles.sh ;;
+        apicopy)
+            step prof_api_copy 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/prof_api_copy -o run --output-format csv -- python tools/api_trace.py run copy
+            python tools/api_trace.py overlap gpurun_out/prof_api_copy/run_kernel_trace.csv gpurun_out/prof_api_copy/run_memory_copy_trace.csv --out gpurun_out/api_copy_overlap.json ;;
+        apiab) for r in 1 2; do for m in 0 1; do PT_SPEC_COPY_FIRST=$m step api_ab_${m}_$r 200 python -c "
+import sys, json; sys.argv=['bench.py']; import bench, os
+sys.path.insert(0, bench.PKG); import ptamd
+tr = ptamd.PathTracer(ptamd.SceneFile(bench.SCENE)); tr.trace_frames(1, 5); tr.synchronize()
+print(json.dumps({'copy_first': os.environ.get('PT_SPEC_COPY_FIRST'), **bench.api_frame_ms(tr, 100)}))" ; done; done ;;
+        benchapi) step bench_api 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-spread ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
