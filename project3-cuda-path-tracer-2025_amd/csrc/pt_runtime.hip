@@ -25,6 +25,9 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -1140,8 +1143,13 @@ void launch(int kind, K kernel, dim3 grid, dim3 block, uint32_t lds, A... args) 
 }
 int nblocks(int n) { return (n + BLOCK - 1) / BLOCK; }
 
+int spec_worker_idle();
 void release_graph() {
-    if (gp->spec_exec) (void)hipGraphExecDestroy(gp->spec_exec);
+    if (gp->spec_exec) {   // the launcher may still be queueing it, the stream still running it
+        (void)spec_worker_idle();
+        (void)hipStreamSynchronize(gp->spec_stream);
+        (void)hipGraphExecDestroy(gp->spec_exec);
+    }
     if (gp->spec_graph) (void)hipGraphDestroy(gp->spec_graph);
     gp->spec_exec = nullptr;
     gp->spec_graph = nullptr;
@@ -1425,6 +1433,86 @@ int run_frame(int iter) { return run_pass(iter, 1); }
 // passes, the test and profiling entry points) first waits for it and drops it (spec_cancel).
 // Only calls that copy the image out start one.  PT_SPECULATE=0 turns it off.  One device
 // context, fused pipeline.
+// The speculative frame is queued by a launcher thread: the copy into the caller's pageable memory
+// holds the calling thread for its whole ~0.14 ms, so the frame must be queued before it -- and
+// queueing it on the calling thread (event wait + graph launch, ~20 us of host time) delayed the
+// copy by as much.  The caller records spec_ev_in, hands the launcher {stream, graph, events,
+// iteration preset} and goes straight on to the copy; everything that later touches the speculative
+// stream, its events or its graph waits for the launcher first (spec_worker_idle).
+struct SpecLauncher {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool task = false, busy = false, stop = false;
+    hipError_t err = hipSuccess;
+    // the task
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_done = nullptr;
+    hipGraphExec_t exec = nullptr;
+    int* iter_ptr = nullptr;
+    int preset = -1;   // < 0: the iteration is already right
+
+    void run() {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return task || stop; });
+            if (stop) return;
+            task = false;
+            const int dev = device, pre = preset;
+            hipStream_t st = stream;
+            hipEvent_t ei = ev_in, ed = ev_done;
+            hipGraphExec_t ex = exec;
+            int* ip = iter_ptr;
+            lk.unlock();
+            hipError_t e = hipSetDevice(dev);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, ei, 0);
+            if (e == hipSuccess && pre >= 0) e = hipMemsetD32Async((hipDeviceptr_t)ip, pre, 1, st);
+            if (e == hipSuccess) e = hipGraphLaunch(ex, st);
+            if (e == hipSuccess) e = hipEventRecord(ed, st);
+            lk.lock();
+            if (e != hipSuccess) err = e;
+            busy = false;
+            cv.notify_all();
+        }
+    }
+    void post(int dev, hipStream_t st, hipEvent_t ei, hipEvent_t ed, hipGraphExec_t ex, int* ip, int pre) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!th.joinable()) th = std::thread([this] { run(); });
+        device = dev;
+        stream = st;
+        ev_in = ei;
+        ev_done = ed;
+        exec = ex;
+        iter_ptr = ip;
+        preset = pre;
+        task = busy = true;
+        cv.notify_all();
+    }
+    hipError_t idle() {   // wait until the posted launch is queued; its error, once
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !busy; });
+        const hipError_t e = err;
+        err = hipSuccess;
+        return e;
+    }
+    void join() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        if (th.joinable()) th.join();
+        stop = false;
+    }
+    ~SpecLauncher() { join(); }   // a process that exits without pt_free: an idle thread, stopped
+};
+SpecLauncher g_spec_launcher;
+int spec_worker_idle() {
+    HIPCHK(g_spec_launcher.idle());
+    return PT_OK;
+}
+
 bool spec_enabled() {
     const char* e = getenv("PT_SPECULATE");   // read per call: tests and bench.py compare both
     return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED;
@@ -1432,10 +1520,13 @@ bool spec_enabled() {
 int spec_cancel() {
     if (gp->spec_iter == 0) return PT_OK;
     gp->spec_iter = 0;
+    RC(spec_worker_idle());
     HIPCHK(hipStreamSynchronize(gp->spec_stream));
     return PT_OK;
 }
 void spec_release() {
+    (void)g_spec_launcher.idle();
+    if (gp == &g_primary) g_spec_launcher.join();
     if (gp->spec_stream) (void)hipStreamSynchronize(gp->spec_stream);
     if (gp->spec_ev_in) (void)hipEventDestroy(gp->spec_ev_in);
     if (gp->spec_ev_done) (void)hipEventDestroy(gp->spec_ev_done);
@@ -1459,6 +1550,7 @@ int spec_launch(int iter) {
         HIPCHK(hipMemsetAsync(gp->d_ctl_spec, 0, sizeof(FrameCtl), gp->spec_stream));
         HIPCHK(hipMalloc((void**)&gp->d_spec_plane, sizeof(float) * 3 * (size_t)gp->pixels_total));
     }
+    RC(spec_worker_idle());   // the launcher is done with the previous launch (events, graph)
     if (!gp->spec_exec) {   // captured once (released with the pass graphs: camera, depth, buffers)
         hipStream_t main_stream = gp->stream;
         FrameCtl* main_ctl = gp->d_ctl;
@@ -1478,23 +1570,21 @@ int spec_launch(int iter) {
         gp->spec_graph = gr;
         HIPCHK(hipGraphInstantiate(&gp->spec_exec, gr, nullptr, nullptr, 0));
     }
-    // behind gp->stream's work so far; ONE graph launch, so that the image copy the caller queues
-    // next starts without waiting for the host to launch six kernels
+    // behind gp->stream's work so far, as ONE graph launch queued by the launcher thread, so that
+    // the image copy the caller queues next starts at once.  The captured k_frame_begin advances the
+    // speculative FrameCtl's iteration by one: it is preset only when the last speculative frame was
+    // not iter - 1 (consecutive calls launch the graph alone)
     HIPCHK(hipEventRecord(gp->spec_ev_in, gp->stream));
-    HIPCHK(hipStreamWaitEvent(gp->spec_stream, gp->spec_ev_in, 0));
-    // the captured k_frame_begin advances the speculative FrameCtl's iteration by one: preset it
-    // only when the last speculative frame was not iter - 1 (consecutive calls launch the graph alone)
-    if (gp->spec_dev_iter != iter - 1)
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&gp->d_ctl_spec->iter, iter - 1, 1, gp->spec_stream));
-    HIPCHK(hipGraphLaunch(gp->spec_exec, gp->spec_stream));
+    g_spec_launcher.post(gp->device, gp->spec_stream, gp->spec_ev_in, gp->spec_ev_done, gp->spec_exec,
+                         &gp->d_ctl_spec->iter, gp->spec_dev_iter != iter - 1 ? iter - 1 : -1);
     gp->spec_dev_iter = iter;
-    HIPCHK(hipEventRecord(gp->spec_ev_done, gp->spec_stream));
     gp->spec_iter = iter;
     return PT_OK;
 }
 // the call for the speculative frame's iteration: take it over on gp->stream
 int spec_adopt() {
     const int iter = gp->spec_iter;
+    RC(spec_worker_idle());   // spec_ev_done recorded
     HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
     const int items = gp->sc.shard.mode != PT_SHARD_PIXELS ? (3 * gp->local_pixels + 3) / 4 : gp->local_pixels;
     launch(7, k_adopt_frame, dim3(nblocks(items)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane, gp->d_image,
@@ -3162,7 +3252,10 @@ int32_t pt_prepare_frames(int32_t count) {
 
 int32_t pt_synchronize(void) {
     RC(need_init());
-    if (g_primary.spec_stream) HIPCHK(hipStreamSynchronize(g_primary.spec_stream));   // it stays valid
+    if (g_primary.spec_stream) {   // it stays valid
+        HIPCHK(g_spec_launcher.idle());
+        HIPCHK(hipStreamSynchronize(g_primary.spec_stream));
+    }
     for (int k = nshards() - 1; k >= 0; --k) {
         ShardScope sc(shard_ctx(k));
         HIPCHK(hipStreamSynchronize(gp->stream));
