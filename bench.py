@@ -392,7 +392,9 @@ def sub_config(ptamd, cfg):
            "roofline": roofline(prof, st_prof, pipeline, steps, d, False,
                                 traffic_file=("c4_bunny" if "bnnuy" in scene_name and res is None else
                                               "c5_khaslana" if "khaslana" in scene_name and res == (1600, 1600)
-                                              and depth == 12 else None)),
+                                              and depth == 12 else
+                                              "staged_c2" if pipeline == "staged" and "glass" in scene_name and sort
+                                              else None)),
            "kernels": kernels_digest(prof, None)}
     if tag == "configs[4]":
         out["note"] = "BASELINE names 8 GPUs for this config; this sub-record is one GPU (bench.py --gpus 8 --scene ...)"
@@ -496,8 +498,8 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
     if traffic_file:
         # a config with its own committed PMC digest (profiles/rNN_traffic_<tag>.json): both
         # kernels of a bounce, bytes per frame scaled to this run's frames per launch pair
-        per_frame = sum(v.get("hbm_bytes_per_frame", 0) for k, v in _pmc_digest(traffic_file).items()
-                        if k in ("k_bounce", "k_bvh_bounce"))
+        keys = ("k_bounce", "k_bvh_bounce") if pipeline == "fused" else ("k_compact_scatter",)
+        per_frame = sum(v.get("hbm_bytes_per_frame", 0) for k, v in _pmc_digest(traffic_file).items() if k in keys)
         traffic = int(per_frame * steps / launches) if per_frame else None
     line = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
