@@ -164,6 +164,9 @@ def inproc_child(args, world):
     reference's callers get.  A child process with a time limit: its failure is recorded, not fatal."""
     cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--inproc", "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--scene", args.scene]
+    # PT_BENCH_INPROC_DEVICES (e.g. "0,0"): the device list for a rehearsal with ranks sharing one GPU
+    if os.environ.get("PT_BENCH_INPROC_DEVICES"):
+        cmd += ["--inproc-devices", os.environ["PT_BENCH_INPROC_DEVICES"]]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                                               "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
     try:
@@ -332,7 +335,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if world > 1:
         dist.destroy_process_group()
-        if rank == 0 and backend == "nccl" and not args.no_inproc:
+        if rank == 0 and not args.no_inproc and (backend == "nccl" or os.environ.get("PT_BENCH_INPROC_DEVICES")):
             line["inproc"] = inproc_child(args, world)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -715,7 +715,7 @@ def test_bench_two_ranks_pixel_tiles(tmp_path, oracle):
     (gloo, sharing this GPU), each traces its interleaved row bands of 2 x (W + K) frames, rank 0
     gathers the tiles; the line reports n_gpus 2 and the image is bit-identical to one GPU's."""
     dump = tmp_path / "img.npy"
-    env = dict(os.environ, PT_BENCH_BACKEND="gloo")
+    env = dict(os.environ, PT_BENCH_BACKEND="gloo", PT_BENCH_INPROC_DEVICES="0,0")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup",
@@ -725,6 +725,10 @@ def test_bench_two_ranks_pixel_tiles(tmp_path, oracle):
     line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["distributed"]["world_size"] == 2
     assert line["scaling"] == "weak" and line["distributed"]["shard"] == "pixels"
+    # rank 0's follow-up: the same N as ONE process behind one pathtrace() (here both shards on GPU 0)
+    ip = line["inproc"]
+    assert ip.get("mode") == "inproc" and ip["n_gpus"] == 2 and ip["devices"] == [0, 0], ip
+    assert ip["value"] > 0 and ip["ms_per_step"] > 0 and ip["api_ms_per_frame"] > 0
     a = oracle.load_scene(scene_path("cornell"))
     r = oracle.Renderer(a, oracle.options(**BIT))
     for it in range(1, 2 * (1 + 3) + 1):
