@@ -1074,6 +1074,7 @@ struct State {
     int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
     int spec_dev_iter = 0;                // d_ctl_spec->iter after the speculative frames queued so far
     int key_bits = 1;
+    bool multi = false;              // a shard context of a multi-device pt_init
 };
 State g_primary;                 // the process's context (shard 0 of a multi-device context)
 State* gp = &g_primary;          // the context the host runtime works on now (see ShardScope)
@@ -1403,8 +1404,12 @@ int run_pass(int iter, int batch) {
     // a single-frame pass (the API's pathtrace(), one call per frame) is launched directly: its six
     // kernels run back to back either way, and a graph launch costs the host ~10 us more before
     // its first kernel starts (tools/api_trace.py; PT_F1_GRAPH=1 keeps the graph, A/B)
+    // Shards of a multi-device context replay their single-frame pass as a graph too: there the
+    // host walks the shards one after another, and one graph launch per shard costs the host less
+    // than six kernel launches (tools/multi_probe.py enqueue_us_per_shard)
     static const bool f1_graph = getenv("PT_F1_GRAPH") && atoi(getenv("PT_F1_GRAPH")) != 0;
-    if (gp->opts.use_graph && (batch > 1 || f1_graph)) {
+    static const bool multi_direct = getenv("PT_MULTI_F1_DIRECT") && atoi(getenv("PT_MULTI_F1_DIRECT")) != 0;  // A/B
+    if (gp->opts.use_graph && (batch > 1 || f1_graph || (gp->multi && !multi_direct))) {
         if (!gp->graph_exec[batch]) RC(build_graph(batch));
         // the graph's k_frame_begin advances the device iteration by one: preset iter - 1 (stream-
         // ordered) unless the last pass left it there -- main.cpp's pathtrace(pbo, 0, ++iteration)
@@ -3114,6 +3119,7 @@ int32_t pt_init(const pt_scene_view* s, const pt_options* opts_in) {
         for (int j = 0; j < n; ++j) share += o.device_ids[j] == o.device_ids[k];
         ShardScope sc(M.shard[k]);
         rc = init_one(s, ok, share);
+        gp->multi = true;
     }
     if (rc == PT_OK) rc = multi_setup();
     if (rc != PT_OK) {

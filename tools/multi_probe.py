@@ -77,6 +77,8 @@ def main():
         out["passes"][key] = passes(ptamd, sc, k, devices=[0] * n, combine=comb)
         out["api"][key] = api(ptamd, sc, devices=[0] * n, combine=comb)
     out["enqueue_us_per_shard"] = {}
+    if os.environ.get("PT_MULTI_F1_DIRECT"):
+        out["note"] = "PT_MULTI_F1_DIRECT=1: single-frame passes of shards launched directly (no graph)"
     for n in (1, 2, 8):
         for f in (1, 20):
             kw = {} if n == 1 else {"devices": [0] * n}

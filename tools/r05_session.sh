@@ -29,6 +29,7 @@ for s in "$@"; do
         bench) step bench_k20 400 python bench.py --steps 20 --warmup 5 ;;
         benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
         multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
+        multidirect) PT_MULTI_F1_DIRECT=1 step multi_probe_direct 300 python tools/multi_probe.py 20 ;;
         inproc) step inproc 200 python bench.py --gpus 2 --inproc --inproc-devices 0,0 --steps 20 --warmup 5 ;;
         ab_*)   # ab_<tag>: AB_LIBS / AB_ROUNDS from the environment, scenes below
             tag=${s#ab_}
