@@ -74,11 +74,6 @@ struct SceneDev {
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
-    // PT_BVH_Q16: the inner records as 2 uint4 each (pair_q16) and the grid their child boxes are
-    // quantised on: world = q_lo + q * q_cell per axis, q a 16-bit integer
-    const uint4* pq;
-    float q_lo[3], q_cell[3];
-    float cull_2_over_E;      // 2 / cull_E rounded up (pair_q16's per-child d from A)
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
@@ -439,33 +434,9 @@ PT_DEV float cull_threshold_packed(float entry, float w) {
     return __builtin_fmaxf(__builtin_fmaf(-d, x, x), 0.0f);
 }
 
-// PT_BVH_Q16 (A/B): 32-B inner records instead of DevPair's 64 B -- two dwordx4 loads per inner
-// step instead of four.  Each child box is quantised OUTWARD on one scene-wide 16-bit grid (per axis
-// q_lo + q * q_cell, q in 0..65535) and padded by m = 2e-5 x the scene extent (pt_init), far more
-// than the float error of the slab distances below (~1e-6 x extent) and of the reference's own box
-// test, so the quantised box passes whenever the reference's test passes on any leaf box inside
-// it: inner decisions are conservative, and the EXACT decision on the reference's leaf box moves
-// to the leaf itself (its box stored with its triangles).  Slab distances come straight from the
-// integers: t = fma(q, q_cell * rr, (q_lo - ro) * rr) per coordinate, with the two factors computed
-// once per ray (qa, qb), so a child costs a convert and an fma per coordinate and no ambiguity
-// branch.  Cull constants: A per child (16 bits, rounded up, as DevPair's), d from A
-// (d <= 2A / E + 3e-6 bounds cull_threshold_packed's d from above: smaller T, never a wrong cull).
-//   a.x = l_lo.x | l_lo.y << 16   a.y = l_lo.z | l_hi.x << 16   a.z = l_hi.y | l_hi.z << 16
-//   a.w = r_lo.x | r_lo.y << 16   b.x = r_lo.z | r_hi.x << 16   b.y = r_hi.y | r_hi.z << 16
-//   b.z = left ref | right ref << 16                             b.w = A_right | A_left << 16
-#ifndef PT_BVH_Q16
-#define PT_BVH_Q16 0
-#endif
-
 // traversal state of one ray on the pair layout
 struct TravState {
-#if PT_BVH_Q16
-    f3 ro, rd;
-    f3 qa, qb;             // per axis q_cell * rr, (q_lo - ro) * rr; rr itself is recomputed where
-                           // needed (the leaf's exact box, slow waves): three registers fewer
-#else
     f3 ro, rd, rr;
-#endif
     float t_hit, bu, bv;   // t_hit starts at t_limit (the primitives' t): see trav_begin
     int btri, cur, sp;
     float curT;   // certified cull threshold of st.cur (0: none)
@@ -480,13 +451,7 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
     const bool par = __builtin_fabsf(rd.x) < 0.00001f || __builtin_fabsf(rd.y) < 0.00001f ||
                      __builtin_fabsf(rd.z) < 0.00001f;
     st.wfast = __all(!(st.exact || par));
-    const f3 rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-#if PT_BVH_Q16
-    st.qa = mk(sc.q_cell[0] * rr.x, sc.q_cell[1] * rr.y, sc.q_cell[2] * rr.z);
-    st.qb = mk((sc.q_lo[0] - ro.x) * rr.x, (sc.q_lo[1] - ro.y) * rr.y, (sc.q_lo[2] - ro.z) * rr.z);
-#else
-    st.rr = rr;
-#endif
+    st.rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
     // t_hit starts at the primitives' t_limit instead of FLT_MAX: the culls used min(t_hit,
     // t_limit), which is then t_hit itself, and a triangle farther than t_limit can never win (the
     // primitive keeps ties, make_hit's strict `<`), so the result is the same and the traversal
@@ -497,7 +462,7 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
     st.sp = 0;
     st.curT = 0.f;
     float e0;
-    st.cur = (aabb_decide(sc.root_lo, sc.root_hi, ro, rd, rr, st.exact, e0) &&
+    st.cur = (aabb_decide(sc.root_lo, sc.root_hi, ro, rd, st.rr, st.exact, e0) &&
               !(t_limit < cull_threshold(sc, e0, sc.root_hi.w)))
                  ? sc.root_ref
                  : -1;
@@ -519,59 +484,6 @@ PT_DEV void trav_pop(TravState& st, int* stack) {
 // expand the internal node st.cur: both child boxes decided exactly (aabb_fast / aabb_decide),
 // certified culls, the nearer passing child continues (true) and the farther one is pushed;
 // false: no child passes (the caller pops)
-#if PT_BVH_Q16
-PT_DEV float q16lo(uint32_t w) { return (float)(w & 0xffffu); }
-PT_DEV float q16hi(uint32_t w) { return (float)(w >> 16); }
-// conservative slab test of one quantised child box (wave-uniform fast path: finite ray, |d| >= 1e-5)
-PT_DEV bool q16_box_fast(const TravState& st, float lx, float ly, float lz, float hx, float hy, float hz,
-                         float& entry) {
-    const float t1x = __builtin_fmaf(lx, st.qa.x, st.qb.x), t2x = __builtin_fmaf(hx, st.qa.x, st.qb.x);
-    const float t1y = __builtin_fmaf(ly, st.qa.y, st.qb.y), t2y = __builtin_fmaf(hy, st.qa.y, st.qb.y);
-    const float t1z = __builtin_fmaf(lz, st.qa.z, st.qb.z), t2z = __builtin_fmaf(hz, st.qa.z, st.qb.z);
-    const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)),
-                                       __builtin_fminf(t1z, t2z));
-    const float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)),
-                                       __builtin_fmaxf(t1z, t2z));
-    entry = tmin;
-    return tmax >= tmin && tmax >= 0.0f;
-}
-// any other ray: the box decoded to world coordinates (its float rounding is far inside the
-// padding) and decided with the reference's arithmetic -- monotone in the bounds, so a superset
-PT_DEV bool q16_box_slow(const SceneDev& sc, const TravState& st, float lx, float ly, float lz, float hx, float hy,
-                         float hz, float& entry) {
-    const float4 lo = make_float4(__builtin_fmaf(lx, sc.q_cell[0], sc.q_lo[0]), __builtin_fmaf(ly, sc.q_cell[1], sc.q_lo[1]),
-                                  __builtin_fmaf(lz, sc.q_cell[2], sc.q_lo[2]), 0.f);
-    const float4 hi = make_float4(__builtin_fmaf(hx, sc.q_cell[0], sc.q_lo[0]), __builtin_fmaf(hy, sc.q_cell[1], sc.q_lo[1]),
-                                  __builtin_fmaf(hz, sc.q_cell[2], sc.q_lo[2]), 0.f);
-    const f3 rr = mk(__builtin_amdgcn_rcpf(st.rd.x), __builtin_amdgcn_rcpf(st.rd.y), __builtin_amdgcn_rcpf(st.rd.z));
-    return aabb_decide(lo, hi, st.ro, st.rd, rr, st.exact, entry);
-}
-// cull_threshold_packed with d bounded from A (see PT_BVH_Q16 above)
-PT_DEV float q16_cull(const SceneDev& sc, float entry, float A) {
-    const float d = __builtin_fmaf(A, sc.cull_2_over_E, 3.1e-6f);
-    const float x = __builtin_fmaf(entry, 1.0f - 2e-6f, -A);
-    return __builtin_fmaxf(__builtin_fmaf(-d, x, x), 0.0f);
-}
-template <bool COUNT = false>
-PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
-    const float t_best = st.t_hit;
-    if (COUNT) n_nodes++;
-    const uint4 a = sc.pq[2 * st.cur], b = sc.pq[2 * st.cur + 1];
-    float el = 0.f, er = 0.f;
-    bool pl, pb;
-    if (st.wfast) {   // wave-uniform
-        pl = q16_box_fast(st, q16lo(a.x), q16hi(a.x), q16lo(a.y), q16hi(a.y), q16lo(a.z), q16hi(a.z), el);
-        pb = q16_box_fast(st, q16lo(a.w), q16hi(a.w), q16lo(b.x), q16hi(b.x), q16lo(b.y), q16hi(b.y), er);
-    } else {
-        pl = q16_box_slow(sc, st, q16lo(a.x), q16hi(a.x), q16lo(a.y), q16hi(a.y), q16lo(a.z), q16hi(a.z), el);
-        pb = q16_box_slow(sc, st, q16lo(a.w), q16hi(a.w), q16lo(b.x), q16hi(b.x), q16lo(b.y), q16hi(b.y), er);
-    }
-    const float Tl = q16_cull(sc, el, __uint_as_float(b.w & 0xffff0000u));
-    const float Tr = q16_cull(sc, er, __uint_as_float(b.w << 16));
-    pl = pl && !(t_best < Tl);
-    pb = pb && !(t_best < Tr);
-    const int rl = (int)(b.z & 0xffffu), rrf = (int)(b.z >> 16);
-#else
 template <bool COUNT = false>
 PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
     const float t_best = st.t_hit;
@@ -597,7 +509,6 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
     pl = pl && !(t_best < Tl);
     pb = pb && !(t_best < Tr);
     const int rl = __float_as_int(pr.l_lo.w), rrf = __float_as_int(pr.r_lo.w);
-#endif
     if (pl && pb) {
         const bool lfirst = el <= er;
         st.cur = lfirst ? rl : rrf;
@@ -626,41 +537,15 @@ PT_DEV void trav_leaf(const SceneDev& sc, TravState& st, int leaf, int& n_nodes,
         n_tris += __float_as_int(sc.hot4[base].c.z);
         sec_add_lanes(SEC_N_LEAVES, 1);
     }
-#if PT_BVH_Q16
-    // the leaf's exact reference box comes with its triangles (11 float4, all loads issued
-    // together): the reference's own decision on it, as the pair layout took it in the parent
-    const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 11 * (size_t)leaf;
-    {
-        const v4f b0 = L[0], b1 = L[1];
-        const float4 blo = make_float4(b0[0], b0[1], b0[2], 0.f), bhi = make_float4(b1[0], b1[1], b1[2], 0.f);
-        float e;
-        bool pass;
-        const f3 rr = mk(__builtin_amdgcn_rcpf(st.rd.x), __builtin_amdgcn_rcpf(st.rd.y), __builtin_amdgcn_rcpf(st.rd.z));
-        if (st.wfast) {
-            bool amb;
-            pass = aabb_fast(blo, bhi, st.ro, rr, e, amb);
-            if (amb) pass = aabb_test(blo, bhi, st.ro, st.rd);
-        } else {
-            pass = aabb_decide(blo, bhi, st.ro, st.rd, rr, st.exact, e);
-        }
-        if (!pass) return;
-    }
-    v4f c[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) c[k] = L[2 + k];
-    constexpr int C0 = 0;
-#else
     const v4f* L = reinterpret_cast<const v4f*>(sc.leaf9) + 9 * (size_t)leaf;
     v4f c[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) c[k] = L[k];
-    constexpr int C0 = 0;
-#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const f3 v0 = mk(c[C0 + 0][i], c[C0 + 1][i], c[C0 + 2][i]);
-        const f3 e1 = mk(c[C0 + 3][i], c[C0 + 4][i], c[C0 + 5][i]);
-        const f3 e2 = mk(c[C0 + 6][i], c[C0 + 7][i], c[C0 + 8][i]);
+        const f3 v0 = mk(c[0][i], c[1][i], c[2][i]);
+        const f3 e1 = mk(c[3][i], c[4][i], c[5][i]);
+        const f3 e2 = mk(c[6][i], c[7][i], c[8][i]);
         float t, u, v;
         if (tri_test_e(st.ro, st.rd, v0, e1, e2, t, u, v) && t > 0.0f &&
             (t < st.t_hit || (t == st.t_hit && base + i < st.btri))) {

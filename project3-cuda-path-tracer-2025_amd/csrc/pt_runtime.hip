@@ -220,28 +220,16 @@ __global__ __launch_bounds__(BLOCK) void k_gather_shards(float* __restrict__ ima
 // --------------------------------------------------------------------------------------------
 // VAR_BVH_SPLIT traversal queue: the path (3 float4 as in PathBuf, C.w = frame slot | (winner
 // geom + 1) << 8) and the primitive result it enters traversal with (t_min, normal seed)
-// PT_QIDX (A/B): the entry names the path instead of copying it -- E = (source, winner geom + 1),
-// D as above -- and k_bvh_bounce gathers the path from the bounce's input segments (read-only
-// while the bounce runs) or, at bounce 0, regenerates the camera ray from its index: 24 B written
-// per queued ray instead of 64
-#ifndef PT_QIDX
-#define PT_QIDX 0
-#endif
 struct QueueBuf {
     float4 *A, *B, *C, *D;   // D = t_min | seed.xyz
-    int2* E;                 // PT_QIDX: source (camera path index at bounce 0, else input slot) | winner + 1
     int stride;              // entries per queue segment (segment s at s * stride, FrameCtl::qcnt)
 };
-// queue entry k for path p (read from input slot / camera index `src`) and its primitive result
-PT_DEV void queue_put(const QueueBuf& q, int k, const PathReg& p, int src, float qt, int qw, f3 qs) {
+// queue entry k for path p and its primitive result
+PT_DEV void queue_put(const QueueBuf& q, int k, const PathReg& p, float qt, int qw, f3 qs) {
+    q.A[k] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
+    q.B[k] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
+    q.C[k] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
     q.D[k] = make_float4(qt, qs.x, qs.y, qs.z);
-    if (PT_QIDX) {
-        q.E[k] = make_int2(src, qw + 1);
-    } else {
-        q.A[k] = make_float4(p.o.x, p.o.y, p.o.z, __int_as_float(p.pix));
-        q.B[k] = make_float4(p.d.x, p.d.y, p.d.z, __int_as_float(p.rb));
-        q.C[k] = make_float4(p.c.x, p.c.y, p.c.z, __int_as_float(p.slot | ((qw + 1) << 8)));
-    }
 }
 
 // Block-aggregated append of up to two flags: ballot -> per-wave counts -> one atomic per flag
@@ -298,22 +286,8 @@ PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i
     i1 = TWO ? s_b[1] + s_w[1][w] + mbcnt(m1) : 0;
 }
 
-// Scalar registers decide how many 256-thread blocks a CU admits, beside VGPRs and LDS:
-// min(8, floor(800 / (ceil(sgpr / 16) * 16 + 16))) (MI355X_MICROARCH.md, Residency) -- 80 SGPRs
-// for 8 blocks, 96 for 7, 112 for 6.  The compiler's occupancy model does not count this, so a
-// kernel whose uniform state grows past 80 SGPRs silently loses blocks.  PT_KB_NUM_SGPR caps
-// k_bounce's (0: no cap).
-#ifndef PT_KB_NUM_SGPR
-#define PT_KB_NUM_SGPR 0
-#endif
-#if PT_KB_NUM_SGPR > 0
-#define PT_KB_SGPR_ATTR __attribute__((amdgpu_num_sgpr(PT_KB_NUM_SGPR)))
-#else
-#define PT_KB_SGPR_ATTR
-#endif
-
 template <bool FIRST, bool HAS_BVH, int VAR>
-__global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
+__global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride,
                                                   QueueBuf q) {
     // dynamic LDS: [geom table, sc.num_geoms <= LDS_GEOMS, candidate-queue variants]
@@ -351,15 +325,13 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
     bool active = gid < n;
     PathReg p;
     p.rb = 0;
-    int src = gid;   // where k_bvh_bounce finds this path again (PT_QIDX): camera index / input slot
     if (active) {
         if (FIRST) {
             const int slot = gid / sc.shard.local_pixels;
             p = camera_ray(sc.cam, iter + slot, sc.trace_depth, shard_pixel(sc, gid - slot * sc.shard.local_pixels));
             p.slot = slot;
         } else {
-            src = segment_slot(segoff, gid, block_start, seg_stride);
-            p = load_path(in, src);
+            p = load_path(in, segment_slot(segoff, gid, block_start, seg_stride));
         }
     }
     // the geom table after the path loads are issued (their latencies overlap); per-lane candidate
@@ -417,7 +389,7 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
             block_append<false>(queued, &ctl->qcnt[bounce][blockIdx.x & (NSEG - 1)][0], false, nullptr, qi, unused);
             qi += (blockIdx.x & (NSEG - 1)) * q.stride;
             if (queued) {
-                queue_put(q, qi, p, src, qt, qw, qs);
+                queue_put(q, qi, p, qt, qw, qs);
                 active = false;   // handed over to k_bvh_bounce
                 live = false;
                 queued = false;
@@ -450,7 +422,7 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
             base = __shfl(base, 0);
             if (queued) {
                 const int k = seg * q.stride + base + mbcnt(mq);
-                queue_put(q, k, p, src, qt, qw, qs);
+                queue_put(q, k, p, qt, qw, qs);
             }
         }
         return;
@@ -460,7 +432,7 @@ __global__ __launch_bounds__(BLOCK) PT_KB_SGPR_ATTR void k_bounce(SceneDev sc, P
     block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
     if (surv) store_path(out, seg * seg_stride + si, p);
     qi += seg * q.stride;
-    if (SPLIT && queued) queue_put(q, qi, p, src, qt, qw, qs);
+    if (SPLIT && queued) queue_put(q, qi, p, qt, qw, qs);
     if (TIMING && active) sec_add(SEC_STORE, sec_clock() - tc);
 }
 
@@ -541,10 +513,48 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #define BVH_WAVES 7
 #endif
 
-template <bool FIRST, int VAR>
-__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf in, PathBuf out,
-                                                                 FrameCtl* ctl, float* __restrict__ image, int bounce,
-                                                                 int seg_stride) {
+// PT_BVH_PART (A/B): each block regroups its queued rays before the traversal -- rays whose origin
+// lies inside the mesh's root box (on or in the mesh: long traversals, most of them hits) after the
+// others (entering from outside: short, mostly misses) -- so that a wave's rays take similar
+// numbers of steps.  Which thread traces a ray changes nothing in its result.
+#ifndef PT_BVH_PART
+#define PT_BVH_PART 0
+#endif
+PT_DEV int partition_queue_block(const SceneDev& sc, const QueueBuf& q, int qs) {
+    __shared__ int s_q[BLOCK];
+    __shared__ int s_w[2][BLOCK / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    bool inside = false;
+    if (qs >= 0) {
+        const float4 a = q.A[qs];
+        inside = a.x >= sc.root_lo.x && a.x <= sc.root_hi.x && a.y >= sc.root_lo.y && a.y <= sc.root_hi.y &&
+                 a.z >= sc.root_lo.z && a.z <= sc.root_hi.z;
+    }
+    const bool c0 = qs >= 0 && !inside, c1 = qs >= 0 && inside;
+    const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+    if (lane == 0) {
+        s_w[0][w] = __popcll(m0);
+        s_w[1][w] = __popcll(m1);
+    }
+    __syncthreads();
+    int tot0 = 0, tot1 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; ++i) {
+        const int x0 = s_w[0][i], x1 = s_w[1][i];
+        tot0 += x0;
+        tot1 += x1;
+        b0 += i < w ? x0 : 0;
+        b1 += i < w ? x1 : 0;
+    }
+    if (c0) s_q[b0 + mbcnt(m0)] = qs;
+    if (c1) s_q[tot0 + b1 + mbcnt(m1)] = qs;
+    __syncthreads();
+    return tid < tot0 + tot1 ? s_q[tid] : -1;
+}
+
+template <int VAR>
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
+                                                                 float* __restrict__ image, int bounce, int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
     int segoff[NSEG + 1];
     segoff[0] = 0;
@@ -558,64 +568,35 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     const int tid = threadIdx.x;
     const int gid = block_start + tid;
+#if PT_BVH_PART
+    const int qs = partition_queue_block(sc, q, gid < n ? segment_slot(segoff, gid, block_start, q.stride) : -1);
+    const bool active = qs >= 0;
+#else
     const bool active = gid < n;
+    const int qs = active ? segment_slot(segoff, gid, block_start, q.stride) : 0;
+#endif
     PathReg p;
     p.rb = 0;
     if (active) {
         // traversal needs only the ray and its primitive t; the rest of the path is fetched
         // afterwards (fewer registers live across the traversal loop -> occupancy)
-        const int qs = segment_slot(segoff, gid, block_start, q.stride);
+        const float4 a = q.A[qs], b = q.B[qs];
         const float t_prim = q.D[qs].x;
-        if (PT_QIDX) {
-            const int src = q.E[qs].x;
-            if (FIRST) {   // the camera ray again, from its path index (bit-identical: same function)
-                const int slot = src / sc.shard.local_pixels;
-                const PathReg c = camera_ray(sc.cam, iter + slot, sc.trace_depth,
-                                             shard_pixel(sc, src - slot * sc.shard.local_pixels));
-                p.o = c.o;
-                p.d = c.d;
-            } else {
-                const float4 a = in.A[src], b = in.B[src];
-                p.o = mk(a.x, a.y, a.z);
-                p.d = mk(b.x, b.y, b.z);
-            }
-        } else {
-            const float4 a = q.A[qs], b = q.B[qs];
-            p.o = mk(a.x, a.y, a.z);
-            p.d = mk(b.x, b.y, b.z);
-        }
+        p.o = mk(a.x, a.y, a.z);
+        p.d = mk(b.x, b.y, b.z);
         float u = 0.f, v = 0.f;
         int tri = -1;
         constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
         const float tb = bvh_intersect_pairs<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
         // the other words re-read here (L2): reading every word once, before the traversal,
         // keeps 5 more registers live across it -- bunny +6.7 %, khaslana +5.5 % (A/B, round 3)
-        const float4 d = q.D[qs];
-        int win;
-        if (PT_QIDX) {
-            const int2 e = q.E[qs];
-            win = e.y - 1;
-            if (FIRST) {
-                p.slot = e.x / sc.shard.local_pixels;
-                p.pix = shard_pixel(sc, e.x - p.slot * sc.shard.local_pixels);
-                p.rb = sc.trace_depth;
-                p.c = mk(1.f, 1.f, 1.f);
-            } else {
-                const float4 c = in.C[e.x];
-                p.pix = __float_as_int(in.A[e.x].w);
-                p.rb = __float_as_int(in.B[e.x].w);
-                p.c = mk(c.x, c.y, c.z);
-                p.slot = __float_as_int(c.w);
-            }
-        } else {
-            const float4 c = q.C[qs];
-            p.pix = __float_as_int(q.A[qs].w);
-            p.rb = __float_as_int(q.B[qs].w);
-            p.c = mk(c.x, c.y, c.z);
-            const int cw = __float_as_int(c.w);
-            p.slot = cw & 255;
-            win = (cw >> 8) - 1;
-        }
+        const float4 c = q.C[qs], d = q.D[qs];
+        p.pix = __float_as_int(q.A[qs].w);
+        p.rb = __float_as_int(q.B[qs].w);
+        p.c = mk(c.x, c.y, c.z);
+        const int cw = __float_as_int(c.w);
+        p.slot = cw & 255;
+        const int win = (cw >> 8) - 1;
         const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
         shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
     }
@@ -1031,7 +1012,6 @@ struct State {
     DevPair* d_pairs = nullptr;
     DevTriHot* d_hot4 = nullptr;
     float4* d_leaf9 = nullptr;
-    uint4* d_pq = nullptr;           // PT_BVH_Q16 inner records
     DevTriCold* d_cold = nullptr;
     float4* d_path[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     float4* d_hit_nt = nullptr;
@@ -1189,9 +1169,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
            in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
     if (SPLIT)
-        launch(200 + b, k_bvh_bounce<FIRST, VAR>, grid, dim3(BLOCK),
-               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, in, out,
-               gp->d_ctl, gp->d_image, b, gp->seg_stride);
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
+               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, out, gp->d_ctl,
+               gp->d_image, b, gp->seg_stride);
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1797,7 +1777,6 @@ void free_pass_buffers() {
     dfree(gp->queue.B);
     dfree(gp->queue.C);
     dfree(gp->queue.D);
-    dfree(gp->queue.E);
     dfree(gp->d_contrib);
     gp->sc.contrib = nullptr;
     gp->alloc_frames = 0;
@@ -1825,8 +1804,7 @@ int capacity_for(int frames) {
 size_t pass_bytes(int frames, bool staged) {
     const size_t cap = (size_t)capacity_for(frames);
     size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
-    if (gp->split)   // traversal queue
-        b += (PT_QIDX ? sizeof(float4) + sizeof(int2) : 4 * sizeof(float4)) * (size_t)q_stride_for(frames) * NSEG;
+    if (gp->split) b += 4 * sizeof(float4) * (size_t)q_stride_for(frames) * NSEG;   // traversal queue
     if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
     if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
     return b;
@@ -1850,13 +1828,9 @@ int ensure_frames(int frames) {
     if (gp->split) {   // NSEG queue segments, each room for the queued rays of its k_bounce blocks
         gp->queue.stride = q_stride_for(frames);
         const size_t qn = (size_t)gp->queue.stride * NSEG;
-        if (PT_QIDX) {
-            RC(dalloc(&gp->queue.E, qn));
-        } else {
-            RC(dalloc(&gp->queue.A, qn));
-            RC(dalloc(&gp->queue.B, qn));
-            RC(dalloc(&gp->queue.C, qn));
-        }
+        RC(dalloc(&gp->queue.A, qn));
+        RC(dalloc(&gp->queue.B, qn));
+        RC(dalloc(&gp->queue.C, qn));
         RC(dalloc(&gp->queue.D, qn));
     }
     if (frames > 1) RC(dalloc(&gp->d_contrib, (size_t)gp->pixels_total * 3 * frames));
@@ -1903,8 +1877,7 @@ void free_all() {
     release_graph();
     free_pass_buffers();
     void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
-                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid,
-                    gp->d_pq};
+                    gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (gp->stream) (void)hipStreamDestroy(gp->stream);
@@ -2529,8 +2502,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<DevTriHot> hot;
     std::vector<DevTriCold> cold;
     std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
-    std::vector<uint4> pq;           // PT_BVH_Q16 inner records
-    float q16_lo[3] = {0.f, 0.f, 0.f}, q16_cell[3] = {0.f, 0.f, 0.f}, q16_2_over_E = 0.f;
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0;
@@ -2847,68 +2818,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;
-#if PT_BVH_Q16
-                {   // pair_q16 records (pt_kernels.h PT_BVH_Q16): the grid is the root box grown by
-                    // m on every side, 65535 cells per axis, in the floats the device will use
-                    const double m = 2e-5 * cull_extent;
-                    const float rl[3] = {nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z};
-                    const float rh[3] = {nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z};
-                    for (int a = 0; a < 3; ++a) {
-                        float g = (float)((double)rl[a] - m);
-                        if ((double)g > (double)rl[a] - m) g = std::nextafter(g, -HUGE_VALF);
-                        float c = (float)(((double)rh[a] + m - (double)g) / 65535.0);
-                        if ((double)g + 65535.0 * (double)c < (double)rh[a] + m) c = std::nextafter(c, HUGE_VALF);
-                        q16_lo[a] = g;
-                        q16_cell[a] = c;
-                    }
-                    auto quant = [&](float v, int a, bool up) -> uint32_t {
-                        const double x = ((double)v + (up ? m : -m) - (double)q16_lo[a]) / (double)q16_cell[a];
-                        const double q = up ? std::ceil(x) : std::floor(x);
-                        return (uint32_t)std::min(65535.0, std::max(0.0, q));
-                    };
-                    pq.assign(2 * (size_t)P, make_uint4(0, 0, 0, 0));
-                    for (int i = 0; i < P; ++i) {
-                        const DevPair& pr = pairs[i];
-                        const float4* lo[2] = {&pr.l_lo, &pr.r_lo};
-                        const float4* hi[2] = {&pr.l_hi, &pr.r_hi};
-                        uint32_t q[2][6], ref[2], A[2];
-                        for (int k = 0; k < 2; ++k) {
-                            const float l3[3] = {lo[k]->x, lo[k]->y, lo[k]->z}, h3[3] = {hi[k]->x, hi[k]->y, hi[k]->z};
-                            for (int a = 0; a < 3; ++a) {
-                                q[k][a] = quant(l3[a], a, false);
-                                q[k][3 + a] = quant(h3[a], a, true);
-                            }
-                            int rf;
-                            memcpy(&rf, &lo[k]->w, 4);
-                            ref[k] = (uint32_t)rf;
-                            uint32_t w;
-                            memcpy(&w, &hi[k]->w, 4);
-                            A[k] = w >> 16;   // pack_cull's A, already rounded up to 16 bits
-                        }
-                        uint4& x = pq[2 * (size_t)i];
-                        uint4& y = pq[2 * (size_t)i + 1];
-                        x.x = q[0][0] | q[0][1] << 16;
-                        x.y = q[0][2] | q[0][3] << 16;
-                        x.z = q[0][4] | q[0][5] << 16;
-                        x.w = q[1][0] | q[1][1] << 16;
-                        y.x = q[1][2] | q[1][3] << 16;
-                        y.y = q[1][4] | q[1][5] << 16;
-                        y.z = ref[0] | ref[1] << 16;
-                        y.w = A[1] | A[0] << 16;
-                    }
-                    // leaves: the reference's exact box, then the 9 triangle float4
-                    std::vector<float4> l11(11 * (size_t)L);
-                    for (int k = 0; k < L; ++k) {
-                        const DevNode& nd = nodes[leaf_nodes[k]];
-                        l11[11 * (size_t)k] = make_float4(nd.lo.x, nd.lo.y, nd.lo.z, 0.f);
-                        l11[11 * (size_t)k + 1] = make_float4(nd.hi.x, nd.hi.y, nd.hi.z, 0.f);
-                        for (int j = 0; j < 9; ++j) l11[11 * (size_t)k + 2 + j] = leaf9[9 * (size_t)k + j];
-                    }
-                    leaf9.swap(l11);
-                    q16_2_over_E = (float)(2.0 / (double)Ef);
-                    if ((double)q16_2_over_E < 2.0 / (double)Ef) q16_2_over_E = std::nextafter(q16_2_over_E, HUGE_VALF);
-                }
-#endif
             }
         }
         gp->bvh_lds = (size_t)gp->stack_depth * BLOCK * sizeof(int);
@@ -2988,10 +2897,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
             RC(upload(gp->d_hot4, hot4.data(), hot4.size()));
             RC(dalloc(&gp->d_leaf9, leaf9.size()));
             RC(upload(gp->d_leaf9, leaf9.data(), leaf9.size()));
-            if (!pq.empty()) {
-                RC(dalloc(&gp->d_pq, pq.size()));
-                RC(upload(gp->d_pq, pq.data(), pq.size()));
-            }
         }
     }
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
@@ -3052,12 +2957,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.pairs = gp->d_pairs;
     sc.hot4 = gp->d_hot4;
     sc.leaf9 = gp->d_leaf9;
-    sc.pq = gp->d_pq;
-    for (int a = 0; a < 3; ++a) {
-        sc.q_lo[a] = q16_lo[a];
-        sc.q_cell[a] = q16_cell[a];
-    }
-    sc.cull_2_over_E = q16_2_over_E;
     sc.num_pairs = pair_count;
     sc.root_ref = pair_root_ref;
     sc.root_lo = pair_root_lo;
@@ -3189,14 +3088,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     }
     // the next frame, on the second stream, while this one's image is copied out (queued before
     // the copy: a copy into pageable memory may hold the host until it is done)
-    static const bool copy_first = getenv("PT_SPEC_COPY_FIRST") && atoi(getenv("PT_SPEC_COPY_FIRST")) != 0;  // tools: A/B
-    if (!copy_first && spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
-    if (host_image && copy_first) {
-        const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
-        HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
-        if (spec && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
-        host_image = nullptr;
-    }
+    if (spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
     if (host_image) {
         // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new
