@@ -513,45 +513,6 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #define BVH_WAVES 7
 #endif
 
-// PT_BVH_PART (A/B): each block regroups its queued rays before the traversal -- rays whose origin
-// lies inside the mesh's root box (on or in the mesh: long traversals, most of them hits) after the
-// others (entering from outside: short, mostly misses) -- so that a wave's rays take similar
-// numbers of steps.  Which thread traces a ray changes nothing in its result.
-#ifndef PT_BVH_PART
-#define PT_BVH_PART 0
-#endif
-PT_DEV int partition_queue_block(const SceneDev& sc, const QueueBuf& q, int qs) {
-    __shared__ int s_q[BLOCK];
-    __shared__ int s_w[2][BLOCK / 64];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    bool inside = false;
-    if (qs >= 0) {
-        const float4 a = q.A[qs];
-        inside = a.x >= sc.root_lo.x && a.x <= sc.root_hi.x && a.y >= sc.root_lo.y && a.y <= sc.root_hi.y &&
-                 a.z >= sc.root_lo.z && a.z <= sc.root_hi.z;
-    }
-    const bool c0 = qs >= 0 && !inside, c1 = qs >= 0 && inside;
-    const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
-    if (lane == 0) {
-        s_w[0][w] = __popcll(m0);
-        s_w[1][w] = __popcll(m1);
-    }
-    __syncthreads();
-    int tot0 = 0, tot1 = 0, b0 = 0, b1 = 0;
-#pragma unroll
-    for (int i = 0; i < BLOCK / 64; ++i) {
-        const int x0 = s_w[0][i], x1 = s_w[1][i];
-        tot0 += x0;
-        tot1 += x1;
-        b0 += i < w ? x0 : 0;
-        b1 += i < w ? x1 : 0;
-    }
-    if (c0) s_q[b0 + mbcnt(m0)] = qs;
-    if (c1) s_q[tot0 + b1 + mbcnt(m1)] = qs;
-    __syncthreads();
-    return tid < tot0 + tot1 ? s_q[tid] : -1;
-}
-
 template <int VAR>
 __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
                                                                  float* __restrict__ image, int bounce, int seg_stride) {
@@ -568,13 +529,8 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     const int tid = threadIdx.x;
     const int gid = block_start + tid;
-#if PT_BVH_PART
-    const int qs = partition_queue_block(sc, q, gid < n ? segment_slot(segoff, gid, block_start, q.stride) : -1);
-    const bool active = qs >= 0;
-#else
     const bool active = gid < n;
     const int qs = active ? segment_slot(segoff, gid, block_start, q.stride) : 0;
-#endif
     PathReg p;
     p.rb = 0;
     if (active) {
