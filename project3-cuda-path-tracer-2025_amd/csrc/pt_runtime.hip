@@ -130,17 +130,20 @@ __global__ __launch_bounds__(BLOCK) void k_adopt_frame(SceneDev sc, const float*
                                                        float* __restrict__ image, FrameCtl* ctl,
                                                        const FrameCtl* spec, int rows) {
     const int t = threadIdx.x;
-    if (blockIdx.x == 0 && t < rows * NSEG) {   // one thread per (bounce row, segment), all loads at once
-        const bool fold = ctl->frames > 0;        // (frames only grows: a late reader folds the same zeros)
-        int* c = &ctl->cnt[0][0][0] + t * CNT_PAD;
-        int* q = &ctl->qcnt[0][0][0] + t * CNT_PAD;
-        const int c0 = *c, q0 = *q;
-        const int c1 = (&spec->cnt[0][0][0])[t * CNT_PAD], q1 = (&spec->qcnt[0][0][0])[t * CNT_PAD];
-        const int b = t / NSEG;
-        if (fold && c0) atomicAdd(&ctl->tot[b], (unsigned long long)(unsigned)c0);
-        if (fold && q0) atomicAdd(&ctl->qtot[b], (unsigned long long)(unsigned)q0);
-        *c = c1;
-        *q = q1;
+    if (blockIdx.x == 0) {   // one thread per (bounce row, segment): all the loads at once
+        const bool fold = ctl->frames > 0;
+        for (int i = t; i < rows * NSEG; i += BLOCK) {
+            int* c = &ctl->cnt[0][0][0] + i * CNT_PAD;
+            int* q = &ctl->qcnt[0][0][0] + i * CNT_PAD;
+            const int c0 = *c, q0 = *q;
+            const int c1 = (&spec->cnt[0][0][0])[i * CNT_PAD], q1 = (&spec->qcnt[0][0][0])[i * CNT_PAD];
+            const int b = i / NSEG;
+            if (fold && c0) atomicAdd(&ctl->tot[b], (unsigned long long)(unsigned)c0);
+            if (fold && q0) atomicAdd(&ctl->qtot[b], (unsigned long long)(unsigned)q0);
+            *c = c1;
+            *q = q1;
+        }
+        __syncthreads();   // every thread read `frames` before it changes
         if (t == 0) {
             ctl->iter = spec->iter;
             ctl->batch = 1;

@@ -135,3 +135,23 @@ def test_camera_change_drops_the_speculated_frame(oracle, ptamd, monkeypatch):
     t2.trace(4)
     assert _eq(t2.image(), got)
     t2.free()
+
+
+def test_speculated_frames_deep_trace(oracle, ptamd, monkeypatch):
+    """trace depth 40: 41 counter rows x 8 segments -- more counters than k_adopt_frame's block has
+    threads; every row's live count taken over from the speculated frame"""
+    monkeypatch.delenv("PT_SPECULATE", raising=False)
+    a, b = _pair(oracle, ptamd, "cornell_glass_test", (32, 32), depth=40)
+    td = ctypes.c_int32(-7)
+    ptamd.lib.pt_init_data_container(ctypes.byref(td))
+    tr = ptamd.PathTracer(b)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    try:
+        for it in (1, 2, 3, 4, 5):
+            _check_frame(tr, r, a, it, td)
+        st = tr.stats()
+        assert st["frames_total"] == 5
+        assert st["segments_total"] > 0
+    finally:
+        tr.free()
+        ptamd.lib.pt_init_data_container(None)
