@@ -50,6 +50,8 @@ sys.path.insert(0, bench.PKG); import ptamd
 tr = ptamd.PathTracer(ptamd.SceneFile(bench.SCENE)); tr.trace_frames(1, 5); tr.synchronize()
 print(json.dumps({'copy_first': os.environ.get('PT_SPEC_COPY_FIRST'), **bench.api_frame_ms(tr, 100)}))" ; done; done ;;
         benchapi) step bench_api 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-spread ;;
+        trim) for r in 1 2 3; do for t in 0 120; do PT_GRID_TRIM_PCT=$t step trim_${t}_$r 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-api --no-spread; done; done
+            grep -h '^{' gpurun_out/trim_*.log | python -c "import sys,json; [print(json.loads(l)['ms_per_step']) for l in sys.stdin]" ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
