@@ -121,14 +121,30 @@ __global__ __launch_bounds__(BLOCK) void k_combine(SceneDev sc, const FrameCtl* 
     px[2] = b;
 }
 
-// A speculative single frame (spec_*) taken over by the call that asks for it, in one launch:
-// image += its plane (the same float additions, in the same order, as its paths' gathers into the
-// image would have made), and block 0 gives the caller's FrameCtl its counters -- the previous
-// frame folded into the running totals and the speculative frame's live counts in its place, as
-// k_frame_begin and that frame's kernels would have left them.
-__global__ __launch_bounds__(BLOCK) void k_adopt_frame(SceneDev sc, const float* __restrict__ plane,
-                                                       float* __restrict__ image, FrameCtl* ctl,
-                                                       const FrameCtl* spec, int rows) {
+// A speculative single frame (spec_*).  At its end, on its own stream, k_spec_sum forms the image
+// the call for its iteration will return: image + its plane (the same float additions, in the same
+// order, as its paths' gathers into the image would have made), into a buffer of its own -- so
+// that call copies it to the host at once, while k_adopt_frame makes it the image and gives the
+// caller's FrameCtl the frame's counters (the previous frame folded into the running totals and
+// the speculative frame's live counts in its place, as k_frame_begin and that frame's kernels
+// would have left them).  Whole images, as float4 streams (single context, no pixel shards).
+__global__ __launch_bounds__(BLOCK) void k_spec_sum(const float* __restrict__ image, const float* __restrict__ plane,
+                                                    float* __restrict__ out, int nf) {
+    const int i = 4 * (blockIdx.x * BLOCK + threadIdx.x);
+    if (i + 3 < nf) {
+        float4 x = *reinterpret_cast<const float4*>(image + i);
+        const float4 c = *reinterpret_cast<const float4*>(plane + i);
+        x.x += c.x;
+        x.y += c.y;
+        x.z += c.z;
+        x.w += c.w;
+        *reinterpret_cast<float4*>(out + i) = x;
+    } else {
+        for (int k = i; k < nf; ++k) out[k] = image[k] + plane[k];
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_adopt_frame(const float* __restrict__ sum, float* __restrict__ image, int nf,
+                                                       FrameCtl* ctl, const FrameCtl* spec, int rows) {
     const int t = threadIdx.x;
     if (blockIdx.x == 0) {   // one thread per (bounce row, segment): all the loads at once
         const bool fold = ctl->frames > 0;
@@ -151,31 +167,12 @@ __global__ __launch_bounds__(BLOCK) void k_adopt_frame(SceneDev sc, const float*
             ctl->frames += 1;
         }
     }
-    if (sc.shard.mode != PT_SHARD_PIXELS) {   // every pixel: the planes as one float4 stream
-        const int nf = 3 * sc.shard.local_pixels;
-        const int i = 4 * (blockIdx.x * BLOCK + t);
-        if (i + 3 < nf) {
-            float4 x = *reinterpret_cast<const float4*>(image + i);
-            const float4 c = *reinterpret_cast<const float4*>(plane + i);
-            x.x += c.x;
-            x.y += c.y;
-            x.z += c.z;
-            x.w += c.w;
-            *reinterpret_cast<float4*>(image + i) = x;
-        } else {
-            for (int k = i; k < nf; ++k) image[k] += plane[k];
-        }
-        return;
+    const int i = 4 * (blockIdx.x * BLOCK + t);
+    if (i + 3 < nf) {
+        *reinterpret_cast<float4*>(image + i) = *reinterpret_cast<const float4*>(sum + i);
+    } else {
+        for (int k = i; k < nf; ++k) image[k] = sum[k];
     }
-    const int l = blockIdx.x * BLOCK + t;
-    if (l >= sc.shard.local_pixels) return;
-    const size_t pix = 3 * (size_t)shard_pixel(sc, l);
-    float* px = image + pix;
-    const float* c = plane + pix;
-    const float r = px[0] + c[0], g = px[1] + c[1], b = px[2] + c[2];
-    px[0] = r;
-    px[1] = g;
-    px[2] = b;
 }
 
 // Multi-device combine (pt_options.num_devices > 1): shard k owns the pixels
@@ -1008,6 +1005,9 @@ struct State {
     hipEvent_t spec_ev_done = nullptr;    // spec_stream: the speculative frame is finished
     FrameCtl* d_ctl_spec = nullptr;       // its own counters (d_ctl keeps the caller's frame)
     float* d_spec_plane = nullptr;        // its contributions, one float3 per pixel
+    float* d_spec_sum[2] = {nullptr, nullptr};   // image + plane, formed at its end (alternating)
+    int spec_sum_idx = 0;                 // the buffer the pending speculative frame writes
+    hipStream_t copy_stream = nullptr;    // the host copy of a taken-over frame's image
     hipGraph_t spec_graph = nullptr;      // its pass, captured once (released with the pass graphs)
     hipGraphExec_t spec_exec = nullptr;
     int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
@@ -1396,6 +1396,10 @@ struct SpecLauncher {
     hipGraphExec_t exec = nullptr;
     int* iter_ptr = nullptr;
     int preset = -1;   // < 0: the iteration is already right
+    const float* image = nullptr;   // k_spec_sum: image + plane -> sum
+    const float* plane = nullptr;
+    float* sum = nullptr;
+    int nf = 0;
 
     void run() {
         std::unique_lock<std::mutex> lk(mu);
@@ -1408,11 +1412,18 @@ struct SpecLauncher {
             hipEvent_t ei = ev_in, ed = ev_done;
             hipGraphExec_t ex = exec;
             int* ip = iter_ptr;
+            const float *im = image, *pl = plane;
+            float* su = sum;
+            const int n = nf;
             lk.unlock();
             hipError_t e = hipSetDevice(dev);
             if (e == hipSuccess) e = hipStreamWaitEvent(st, ei, 0);
             if (e == hipSuccess && pre >= 0) e = hipMemsetD32Async((hipDeviceptr_t)ip, pre, 1, st);
             if (e == hipSuccess) e = hipGraphLaunch(ex, st);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_spec_sum, dim3(nblocks((n + 3) / 4)), dim3(BLOCK), 0, st, im, pl, su, n);
+                e = hipGetLastError();
+            }
             if (e == hipSuccess) e = hipEventRecord(ed, st);
             lk.lock();
             if (e != hipSuccess) err = e;
@@ -1420,7 +1431,8 @@ struct SpecLauncher {
             cv.notify_all();
         }
     }
-    void post(int dev, hipStream_t st, hipEvent_t ei, hipEvent_t ed, hipGraphExec_t ex, int* ip, int pre) {
+    void post(int dev, hipStream_t st, hipEvent_t ei, hipEvent_t ed, hipGraphExec_t ex, int* ip, int pre,
+              const float* im, const float* pl, float* su, int n) {
         std::lock_guard<std::mutex> lk(mu);
         if (!th.joinable()) th = std::thread([this] { run(); });
         device = dev;
@@ -1430,6 +1442,10 @@ struct SpecLauncher {
         exec = ex;
         iter_ptr = ip;
         preset = pre;
+        image = im;
+        plane = pl;
+        sum = su;
+        nf = n;
         task = busy = true;
         cv.notify_all();
     }
@@ -1459,7 +1475,8 @@ int spec_worker_idle() {
 
 bool spec_enabled() {
     const char* e = getenv("PT_SPECULATE");   // read per call: tests and bench.py compare both
-    return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED;
+    return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED &&
+           gp->sc.shard.mode != PT_SHARD_PIXELS;
 }
 int spec_cancel() {
     if (gp->spec_iter == 0) return PT_OK;
@@ -1477,6 +1494,10 @@ void spec_release() {
     if (gp->spec_stream) (void)hipStreamDestroy(gp->spec_stream);
     if (gp->d_ctl_spec) (void)hipFree(gp->d_ctl_spec);
     if (gp->d_spec_plane) (void)hipFree(gp->d_spec_plane);
+    for (float*& p : gp->d_spec_sum)
+        if (p) (void)hipFree(p), p = nullptr;
+    if (gp->copy_stream) (void)hipStreamSynchronize(gp->copy_stream), (void)hipStreamDestroy(gp->copy_stream);
+    gp->copy_stream = nullptr;
     gp->spec_stream = nullptr;
     gp->spec_ev_in = gp->spec_ev_done = nullptr;
     gp->d_ctl_spec = nullptr;
@@ -1493,6 +1514,8 @@ int spec_launch(int iter) {
         HIPCHK(hipMalloc((void**)&gp->d_ctl_spec, sizeof(FrameCtl)));
         HIPCHK(hipMemsetAsync(gp->d_ctl_spec, 0, sizeof(FrameCtl), gp->spec_stream));
         HIPCHK(hipMalloc((void**)&gp->d_spec_plane, sizeof(float) * 3 * (size_t)gp->pixels_total));
+        for (float*& p : gp->d_spec_sum) HIPCHK(hipMalloc((void**)&p, sizeof(float) * 3 * (size_t)gp->pixels_total));
+        HIPCHK(hipStreamCreateWithFlags(&gp->copy_stream, hipStreamNonBlocking));
     }
     RC(spec_worker_idle());   // the launcher is done with the previous launch (events, graph)
     if (!gp->spec_exec) {   // captured once (released with the pass graphs: camera, depth, buffers)
@@ -1519,20 +1542,25 @@ int spec_launch(int iter) {
     // speculative FrameCtl's iteration by one: it is preset only when the last speculative frame was
     // not iter - 1 (consecutive calls launch the graph alone)
     HIPCHK(hipEventRecord(gp->spec_ev_in, gp->stream));
+    gp->spec_sum_idx ^= 1;   // the other buffer: the one the caller may still be copying from is kept
     g_spec_launcher.post(gp->device, gp->spec_stream, gp->spec_ev_in, gp->spec_ev_done, gp->spec_exec,
-                         &gp->d_ctl_spec->iter, gp->spec_dev_iter != iter - 1 ? iter - 1 : -1);
+                         &gp->d_ctl_spec->iter, gp->spec_dev_iter != iter - 1 ? iter - 1 : -1, gp->d_image,
+                         gp->d_spec_plane, gp->d_spec_sum[gp->spec_sum_idx], 3 * gp->pixels_total);
     gp->spec_dev_iter = iter;
     gp->spec_iter = iter;
     return PT_OK;
 }
 // the call for the speculative frame's iteration: take it over on gp->stream
-int spec_adopt() {
+// on gp->stream (its image and counters) -- and, when the caller copies the image out, the copy
+// stream waits for it too: the copy reads the finished sum at once, beside k_adopt_frame
+int spec_adopt(bool copy_out) {
     const int iter = gp->spec_iter;
     RC(spec_worker_idle());   // spec_ev_done recorded
     HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
-    const int items = gp->sc.shard.mode != PT_SHARD_PIXELS ? (3 * gp->local_pixels + 3) / 4 : gp->local_pixels;
-    launch(7, k_adopt_frame, dim3(nblocks(items)), dim3(BLOCK), 0, gp->sc, (const float*)gp->d_spec_plane, gp->d_image,
-           gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
+    if (copy_out) HIPCHK(hipStreamWaitEvent(gp->copy_stream, gp->spec_ev_done, 0));
+    const int nf = 3 * gp->pixels_total;
+    launch(7, k_adopt_frame, dim3(nblocks((nf + 3) / 4)), dim3(BLOCK), 0, (const float*)gp->d_spec_sum[gp->spec_sum_idx],
+           gp->d_image, nf, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
     HIPCHK(hipGetLastError());
     gp->spec_iter = 0;
     gp->dev_iter = iter;
@@ -3029,10 +3057,13 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     // speculate only for callers that copy the image out (main.cpp's pathtrace() always does): a
     // call without the copy has nothing for the next frame to overlap with
     const bool spec = M.n <= 1 && spec_enabled() && (host_image != nullptr || gp->spec_iter == iteration);
+    bool adopted = false;
+    const int sum_idx = gp->spec_sum_idx;   // the taken-over frame's image, before the next launch flips it
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (spec && gp->spec_iter == iteration) {
-            RC(spec_adopt());          // traced already, during the previous call's image copy
+            adopted = true;
+            RC(spec_adopt(host_image != nullptr));   // traced already, during the previous call's copy
         } else {
             RC(spec_cancel());
             RC(run_frame(iteration));
@@ -3054,11 +3085,15 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         // one at the same address, and on MI355X the pageable copy runs at the pinned rate anyway
         // (tools/copy_probe.py: 7.68 MB in 0.145 ms either way)
         const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
-        HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
+        if (adopted)   // the speculated frame's finished sum, on the copy stream (it waited for it)
+            HIPCHK(hipMemcpyAsync(host_image, gp->d_spec_sum[sum_idx], bytes, hipMemcpyDeviceToHost, gp->copy_stream));
+        else
+            HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
     }
     // one wait: the first device's stream waited for every shard's frame (multi_combine), and each
     // shard queued its counter copy before that
     HIPCHK(hipStreamSynchronize(gp->stream));
+    if (adopted && host_image) HIPCHK(hipStreamSynchronize(gp->copy_stream));
     if (gp->traced_depth) {
         // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770); with
         // shards, the frame ran as long as its longest shard
@@ -3138,6 +3173,7 @@ int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
 
 int32_t pt_set_image(const float* host_in, int64_t n_floats) {
     RC(need_init());
+    RC(spec_cancel());   // its image + plane was formed from the image being replaced
     if (!host_in || n_floats != (int64_t)gp->pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
     for (int k = 0; k < nshards(); ++k) {   // each shard keeps accumulating into its own pixels of it
         ShardScope sc(shard_ctx(k));

@@ -3,7 +3,8 @@
 main.cpp calls pathtrace(pbo, frame, ++iteration) once per frame and the reference copies the
 accumulated image to host memory every call (pathtrace.cu:783).  After tracing frame N the library
 traces frame N + 1 on a second stream -- into a plane and a FrameCtl of its own -- while frame N's
-image is copied out; the call for N + 1 adds that plane to the image and takes over its counters.
+image is copied out, and forms image + plane at its end; the call for N + 1 copies that sum out at
+once while it becomes the image and the frame's counters are taken over.
 These tests drive every way a caller can break the sequence (another iteration, a repeated one, a
 depth change, a camera change, set_image, stats resets, multi-frame passes in between, a PBO) and
 require the image, the PBO, the per-bounce live counts and TracedDepth to equal the oracle's
