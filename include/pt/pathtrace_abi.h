@@ -278,7 +278,9 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
  * iterations (per wave), [9] waves, [10] live lanes, [11] BVH node + leaf visits, [12] leaf
  * triangles, [13] traversed rays, [14] box-decision mismatches (node-array traversal), [15] wave
  * traversal iterations, [16] leaf visits, [17] traversed rays whose mesh hit wins, [18] node
- * visits of the rays whose mesh hit does not win, [19] rays culled at the root; n <= 24.  `reset` zeroes them after the read. */
+ * visits of the rays whose mesh hit does not win, [19] rays culled at the root, [20..35] wave
+ * traversal iterations by active lanes in bins of 4 (1-4, 5-8, ..); n <= 40.  `reset` zeroes
+ * them after the read. */
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset);
 
 #ifdef __cplusplus

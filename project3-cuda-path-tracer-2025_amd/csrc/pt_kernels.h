@@ -117,8 +117,10 @@ struct FrameCtl {
 // per-lane work counters, summed by the first active lane of each wave
 enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EXACT, SEC_N_CAND, SEC_N_ITERS,
        SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS,
-       SEC_N_LEAVES, SEC_N_BVH_HITS, SEC_N_MISS_NODES, SEC_N_ROOT_CULLED, SEC_COUNT };
-constexpr int SEC_SLOTS = 24;
+       SEC_N_LEAVES, SEC_N_BVH_HITS, SEC_N_MISS_NODES, SEC_N_ROOT_CULLED,
+       SEC_BVH_LANES_HIST,                    // 16 bins: wave traversal steps by active lanes (1-4, 5-8, ..)
+       SEC_COUNT = SEC_BVH_LANES_HIST + 16 };
+constexpr int SEC_SLOTS = 40;
 __device__ unsigned long long g_sections[SEC_SLOTS];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
 PT_DEV void sec_add(int k, uint64_t v) {
@@ -443,7 +445,8 @@ struct TravState {
     bool exact;
     bool wfast;   // wave-uniform: every ray of the wave is finite with all |d| >= 1e-5 (aabb_fast)
 };
-PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_limit) {
+// the ray's part of the state (wfast over the lanes that call it together)
+PT_DEV void trav_ray(TravState& st, f3 ro, f3 rd) {
     st.ro = ro;
     st.rd = rd;
     st.exact = !(ro.x - ro.x == 0.f && ro.y - ro.y == 0.f && ro.z - ro.z == 0.f &&
@@ -452,6 +455,9 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
                      __builtin_fabsf(rd.z) < 0.00001f;
     st.wfast = __all(!(st.exact || par));
     st.rr = mk(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
+}
+PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_limit) {
+    trav_ray(st, ro, rd);
     // t_hit starts at the primitives' t_limit instead of FLT_MAX: the culls used min(t_hit,
     // t_limit), which is then t_hit itself, and a triangle farther than t_limit can never win (the
     // primitive keeps ties, make_hit's strict `<`), so the result is the same and the traversal
@@ -580,6 +586,41 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
     return st.t_hit;
 }
 
+// A ray's traversal handed from one wave to another (k_bvh_bounce -> k_bvh_tail): the best hit so
+// far, the node to expand next and the stack.  The culls' thresholds ride in the stack entries and
+// the ray's reciprocals, exactness and the wave's fast-box flag are recomputed; which box routine
+// a wave uses never changes a decision, so the resumed traversal visits what the ray would have.
+PT_DEV float4 trav_saved_hit(const TravState& st) {
+    return make_float4(st.t_hit, st.bu, st.bv, __int_as_float(st.btri));
+}
+PT_DEV int trav_saved_node(const TravState& st) { return (st.cur & 0xffff) | (st.sp << 16); }   // refs < 2^16
+PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node) {
+    trav_ray(st, ro, rd);
+    st.t_hit = hit.x;
+    st.bu = hit.y;
+    st.bv = hit.z;
+    st.btri = __float_as_int(hit.w);
+    st.cur = node & 0xffff;
+    st.sp = node >> 16;
+    st.curT = 0.f;
+}
+// expand nodes until the ray is finished (st.cur < 0) or -- defer > 0 -- until no more than
+// `defer` lanes of the wave are still traversing: those stop with st.cur >= 0 (wave steps with a
+// handful of lanes cost a wave slot each for a few lanes of work; k_bvh_tail resumes them 64 to a
+// wave).  Counters (COUNT) as bvh_intersect_pairs', the per-ray ones left to the caller.
+template <bool COUNT = false>
+PT_DEV void trav_run(const SceneDev& sc, TravState& st, int* stack, int defer, int& n_nodes, int& n_tris) {
+    while (st.cur >= 0) {
+        const int lanes = __popcll(__builtin_amdgcn_read_exec());   // wave-uniform
+        if (lanes <= defer) break;
+        if (COUNT) {
+            sec_add(SEC_N_BVH_WITERS, 1);
+            sec_add(SEC_BVH_LANES_HIST + (lanes - 1) / 4, 1);
+        }
+        trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
+    }
+}
+
 template <bool COUNT = false>
 PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, float t_limit, float& bu, float& bv,
                                  int& btri) {
@@ -588,7 +629,10 @@ PT_DEV float bvh_intersect_pairs(const SceneDev& sc, f3 ro, f3 rd, int* stack, f
     trav_begin(sc, st, ro, rd, t_limit);
     if (COUNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
     while (st.cur >= 0) {
-        if (COUNT) sec_add(SEC_N_BVH_WITERS, 1);
+        if (COUNT) {
+            sec_add(SEC_N_BVH_WITERS, 1);
+            sec_add(SEC_BVH_LANES_HIST + (__popcll(__builtin_amdgcn_read_exec()) - 1) / 4, 1);
+        }
         trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
     }
     if (COUNT) {

@@ -63,7 +63,11 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
     }
     __syncthreads();
     for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->cnt[0][0][0])[i * CNT_PAD] = 0;
-    for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
+    for (int i = t; i < rows * NSEG; i += blockDim.x) {
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
+#pragma unroll
+        for (int l = 1; l <= 4; ++l) (&ctl->qcnt[0][0][0])[i * CNT_PAD + l] = 0;   // handed-over traversals
+    }
     __syncthreads();
     if (t == 0) {
         ctl->iter = set_iter > 0 ? set_iter : ctl->iter + 1;
@@ -223,6 +227,18 @@ __global__ __launch_bounds__(BLOCK) void k_gather_shards(float* __restrict__ ima
 struct QueueBuf {
     float4 *A, *B, *C, *D;   // D = t_min | seed.xyz
     int stride;              // entries per queue segment (segment s at s * stride, FrameCtl::qcnt)
+};
+// Traversals handed from k_bvh_bounce to k_bvh_tail (see trav_run), and from one k_bvh_tail level
+// to the next: per entry the queue slot and the saved node (trav_saved_node), the best hit so far,
+// and the stack (entry i of e at stack[i * cap + e]).  Segment s (at s * stride; counter
+// FrameCtl::qcnt[b][s][level]) holds the rays of the previous kernel's blocks of segment s, so
+// k_bvh_tail's survivors fit where theirs would have.  Two buffers, levels alternating.
+constexpr int MAX_TAIL_LEVELS = 4;
+struct TailBuf {
+    int2* node;     // queue slot | trav_saved_node
+    float4* hit;    // trav_saved_hit
+    int* stack;
+    int stride, cap;
 };
 // queue entry k for path p and its primitive result
 PT_DEV void queue_put(const QueueBuf& q, int k, const PathReg& p, float qt, int qw, f3 qs) {
@@ -513,9 +529,56 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #define BVH_WAVES 7
 #endif
 
+// after the traversal: the path's other words, the hit, shading (the shared end of k_bvh_bounce
+// and k_bvh_tail)
 template <int VAR>
-__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, PathBuf out, FrameCtl* ctl,
-                                                                 float* __restrict__ image, int bounce, int seg_stride) {
+PT_DEV void bvh_finish_path(const SceneDev& sc, const QueueBuf& q, int qs, int iter, PathReg& p, const TravState& st) {
+    float u = 0.f, v = 0.f;
+    int tri = -1;
+    const float tb = trav_result(st, u, v, tri);
+    // the other words re-read here (L2): reading every word once, before the traversal,
+    // keeps 5 more registers live across it -- bunny +6.7 %, khaslana +5.5 % (A/B, round 3)
+    const float4 c = q.C[qs], d = q.D[qs];
+    p.pix = __float_as_int(q.A[qs].w);
+    p.rb = __float_as_int(q.B[qs].w);
+    p.c = mk(c.x, c.y, c.z);
+    const int cw = __float_as_int(c.w);
+    p.slot = cw & 255;
+    const int win = (cw >> 8) - 1;
+    const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
+    shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+}
+template <bool COUNT>
+PT_DEV void bvh_count_ray(const TravState& st, float t_prim, int n_nodes) {
+    if (COUNT) {
+        sec_add_lanes(SEC_N_BVH_RAYS, 1);
+        const bool hit = st.btri != 0x7fffffff && st.t_hit < t_prim;   // the mesh changes the winner
+        sec_add_lanes(SEC_N_BVH_HITS, hit ? 1 : 0);
+        sec_add_lanes(SEC_N_MISS_NODES, hit ? 0 : n_nodes);   // (a handed-over ray: its tail's nodes)
+    }
+}
+
+// hand the calling lanes' traversals (st.cur >= 0) over to the next level: one atomic per wave.
+// false: the segment is full at this lane's slot -- the caller finishes it itself.  The counter
+// still counts it; every slot below min(counter, stride) is written by the lane that reserved it.
+PT_DEV bool tail_put(const TailBuf& t, int* ctr, int seg, int qs, const TravState& st, const int* s_stack) {
+    const uint64_t m = __ballot(1);
+    const int lead = __builtin_ctzll(m);
+    int base = 0;
+    if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(ctr, __popcll(m));
+    const int slot = __builtin_amdgcn_readlane(base, lead) + mbcnt(m);
+    if (slot >= t.stride) return false;
+    const int e = seg * t.stride + slot;
+    t.node[e] = make_int2(qs, trav_saved_node(st));
+    t.hit[e] = trav_saved_hit(st);
+    for (int i = 0; i < st.sp; ++i) t.stack[(size_t)i * t.cap + e] = s_stack[i * BLOCK];
+    return true;
+}
+
+template <int VAR>
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, TailBuf tail, int defer,
+                                                                 PathBuf out, FrameCtl* ctl, float* __restrict__ image,
+                                                                 int bounce, int seg_stride) {
     extern __shared__ float4 s_dyn[];   // traversal stack, stack_depth x BLOCK ints
     int segoff[NSEG + 1];
     segoff[0] = 0;
@@ -529,7 +592,9 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     const bool to_plane = ctl->batch > 1 || ctl->plane != 0;   // gather into the frame planes
     const int tid = threadIdx.x;
     const int gid = block_start + tid;
+    const int seg = blockIdx.x & (NSEG - 1);
     const bool active = gid < n;
+    bool handed = false;
     const int qs = active ? segment_slot(segoff, gid, block_start, q.stride) : 0;
     PathReg p;
     p.rb = 0;
@@ -540,25 +605,81 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
         const float t_prim = q.D[qs].x;
         p.o = mk(a.x, a.y, a.z);
         p.d = mk(b.x, b.y, b.z);
-        float u = 0.f, v = 0.f;
-        int tri = -1;
         constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
-        const float tb = bvh_intersect_pairs<CNT>(sc, p.o, p.d, s_stack + tid, t_prim, u, v, tri);
-        // the other words re-read here (L2): reading every word once, before the traversal,
-        // keeps 5 more registers live across it -- bunny +6.7 %, khaslana +5.5 % (A/B, round 3)
-        const float4 c = q.C[qs], d = q.D[qs];
-        p.pix = __float_as_int(q.A[qs].w);
-        p.rb = __float_as_int(q.B[qs].w);
-        p.c = mk(c.x, c.y, c.z);
-        const int cw = __float_as_int(c.w);
-        p.slot = cw & 255;
-        const int win = (cw >> 8) - 1;
-        const Hit h = make_hit(sc, p.d, d.x, win, mk(d.y, d.z, d.w), tb, u, v, tri, sc.hot4);
-        shade_path<(VAR & VAR_NO_TEX) == 0>(sc, p, h, iter + p.slot, [&]() { return hit_attr(sc, h); });
+        int n_nodes = 0, n_tris = 0;
+        TravState st;
+        trav_begin(sc, st, p.o, p.d, t_prim);
+        if (CNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
+        trav_run<CNT>(sc, st, s_stack + tid, defer, n_nodes, n_tris);
+        if (st.cur >= 0) {   // handed over: the wave's last few traversals go on 64 to a wave
+            handed = tail_put(tail, &ctl->qcnt[bounce][seg][1], seg, qs, st, s_stack + tid);
+            if (!handed) trav_run<CNT>(sc, st, s_stack + tid, 0, n_nodes, n_tris);   // no room: finish here
+        }
+        if (CNT) {
+            sec_add_lanes(SEC_N_NODES, n_nodes);
+            sec_add_lanes(SEC_N_TRIS, n_tris);
+        }
+        if (!handed) {
+            bvh_count_ray<CNT>(st, t_prim, n_nodes);
+            bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
+        }
     }
-    const bool surv = active && p.rb > 0;
-    if (active && !surv) gather_into_image(image, sc, to_plane, p);
+    const bool surv = active && !handed && p.rb > 0;
+    if (active && !handed && !surv) gather_into_image(image, sc, to_plane, p);
+    int si, unused;
+    block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
+    if (surv) store_path(out, seg * seg_stride + si, p);
+}
+
+// The traversals handed over to `level` (by k_bvh_bounce, or by the previous level), resumed 64
+// to a wave and finished like k_bvh_bounce's own -- or, defer > 0, handed on to level + 1 the same
+// way.  Block (j, s) = blockIdx (j * NSEG + s) takes entries j * BLOCK .. of segment s of `tin`,
+// and its survivors go to output segment s, with those of the blocks the rays came from.
+template <int VAR>
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail(SceneDev sc, QueueBuf q, TailBuf tin, TailBuf tout,
+                                                               int level, int defer, PathBuf out, FrameCtl* ctl,
+                                                               float* __restrict__ image, int bounce, int seg_stride) {
+    extern __shared__ float4 s_dyn[];
     const int seg = blockIdx.x & (NSEG - 1);
+    const int n = min(ctl->qcnt[bounce][seg][level], tin.stride);   // the counter counts refused lanes too
+    const int block_start = (blockIdx.x / NSEG) * BLOCK;
+    if (block_start >= n) return;
+    int* s_stack = reinterpret_cast<int*>(s_dyn);
+    const int iter = ctl->iter;
+    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;
+    const int tid = threadIdx.x;
+    const bool active = block_start + tid < n;
+    bool handed = false;
+    PathReg p;
+    p.rb = 0;
+    if (active) {
+        const int e = seg * tin.stride + block_start + tid;
+        const int2 nd = tin.node[e];
+        const int qs = nd.x;
+        const float4 a = q.A[qs], b = q.B[qs];
+        p.o = mk(a.x, a.y, a.z);
+        p.d = mk(b.x, b.y, b.z);
+        TravState st;
+        trav_resume(st, p.o, p.d, tin.hit[e], nd.y);
+        for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK + tid] = tin.stack[(size_t)i * tin.cap + e];
+        constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
+        int n_nodes = 0, n_tris = 0;
+        trav_run<CNT>(sc, st, s_stack + tid, defer, n_nodes, n_tris);
+        if (st.cur >= 0) {
+            handed = tail_put(tout, &ctl->qcnt[bounce][seg][level + 1], seg, qs, st, s_stack + tid);
+            if (!handed) trav_run<CNT>(sc, st, s_stack + tid, 0, n_nodes, n_tris);   // no room: finish here
+        }
+        if (CNT) {
+            sec_add_lanes(SEC_N_NODES, n_nodes);
+            sec_add_lanes(SEC_N_TRIS, n_tris);
+        }
+        if (!handed) {
+            bvh_count_ray<CNT>(st, q.D[qs].x, n_nodes);
+            bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
+        }
+    }
+    const bool surv = active && !handed && p.rb > 0;
+    if (active && !handed && !surv) gather_into_image(image, sc, to_plane, p);
     int si, unused;
     block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
     if (surv) store_path(out, seg * seg_stride + si, p);
@@ -989,6 +1110,9 @@ struct State {
     bool split = false;              // VAR_BVH_SPLIT active (fused, fast BVH on the pair layout)
     bool no_tex = false;             // no textured / bump-mapped material (VAR_NO_TEX kernels)
     QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
+    TailBuf tail[2] = {};            // the traversals k_bvh_bounce hands to k_bvh_tail (levels alternate)
+    int tail_lanes = 0, tail_levels = 0;   // bvh_tail_lanes(), bvh_tail_levels()
+    int tail_depth = 0;              // stack entries per handed-over traversal
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
     hipGraphExec_t graph_exec[MAXF + 1] = {};
@@ -1127,10 +1251,20 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds + bounce_pad, gp->sc,
            in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
-    if (SPLIT)
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK),
-               (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int) + lds_pad, gp->sc, gp->queue, out, gp->d_ctl,
-               gp->d_image, b, gp->seg_stride);
+    if (SPLIT) {
+        const size_t stack_bytes = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int);
+        // the handed-over stacks were sized for the pair tree of the allocation (ensure_frames)
+        if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
+        const int levels = gp->tail_lanes > 0 ? gp->tail_levels : 0;
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail[0],
+               levels > 0 ? gp->tail_lanes : 0, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
+        for (int l = 1; l <= levels; ++l) {
+            const TailBuf& tin = gp->tail[(l - 1) & 1];
+            launch(400 + b, k_bvh_tail<VAR>, dim3(NSEG * nblocks(tin.stride)), dim3(BLOCK), stack_bytes, gp->sc,
+                   gp->queue, tin, gp->tail[l & 1], l, l < levels ? gp->tail_lanes : 0, out, gp->d_ctl, gp->d_image, b,
+                   gp->seg_stride);
+        }
+    }
 }
 template <bool FIRST, bool HAS_BVH>
 void launch_bounce_v(int var, dim3 grid, PathBuf in, PathBuf out, int b) {
@@ -1764,6 +1898,12 @@ void free_pass_buffers() {
     dfree(gp->queue.B);
     dfree(gp->queue.C);
     dfree(gp->queue.D);
+    for (TailBuf& t : gp->tail) {
+        dfree(t.node);
+        dfree(t.hit);
+        dfree(t.stack);
+        t.stride = t.cap = 0;
+    }
     dfree(gp->d_contrib);
     gp->sc.contrib = nullptr;
     gp->alloc_frames = 0;
@@ -1782,6 +1922,30 @@ int q_stride_for(int frames) {
     const int nb = nblocks(std::max(1, gp->local_pixels * frames));
     return ((nb + NSEG - 1) / NSEG) * BLOCK;
 }
+// k_bvh_bounce hands a wave's traversals to k_bvh_tail once no more than this many of its lanes
+// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 32)
+int bvh_tail_lanes() {
+    const char* e = getenv("PT_BVH_TAIL_LANES");
+    return std::min(32, std::max(0, e ? atoi(e) : 16));
+}
+// ... in up to this many k_bvh_tail levels, the last one finishing every traversal
+// (PT_BVH_TAIL_LEVELS, 1 .. MAX_TAIL_LEVELS)
+int bvh_tail_levels() {
+    const char* e = getenv("PT_BVH_TAIL_LEVELS");
+    return std::min(MAX_TAIL_LEVELS, std::max(1, e ? atoi(e) : 1));
+}
+// entries per segment of tail buffer k: what the kernel filling it can hand over -- `lanes` per
+// wave of its blocks of one segment (k_bvh_bounce: buffer 0; a level reading buffer 0: buffer 1;
+// the levels after that shrink).  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane
+// that finds its segment full then finishes its ray itself (tail_put).  A cap measured slower at
+// every size tried: bunny's passes hand over ~10 % of 128 frames' rays (DESIGN Appendix A).
+int tail_stride(int k, int frames, int lanes) {
+    const char* e = getenv("PT_BVH_TAIL_CHUNKS");
+    const int nb = nblocks(std::max(1, gp->local_pixels * frames));
+    const int s0 = ((nb + NSEG - 1) / NSEG) * (BLOCK / 64) * lanes;
+    const int s = k == 0 ? s0 : nblocks(s0) * (BLOCK / 64) * lanes;
+    return e && atoi(e) > 0 ? std::min(s, atoi(e) * BLOCK) : s;
+}
 // paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
 int capacity_for(int frames) {
     const int c = std::max(seg_stride_for(frames) * NSEG, gp->local_pixels * frames);
@@ -1792,6 +1956,10 @@ size_t pass_bytes(int frames, bool staged) {
     const size_t cap = (size_t)capacity_for(frames);
     size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
     if (gp->split) b += 4 * sizeof(float4) * (size_t)q_stride_for(frames) * NSEG;   // traversal queue
+    if (gp->split && bvh_tail_lanes() > 0)   // handed-over traversals
+        b += (sizeof(int2) + sizeof(float4) + sizeof(int) * std::max(1, gp->sc.pair_stack_depth)) * NSEG *
+             (size_t)(tail_stride(0, frames, bvh_tail_lanes()) +
+                      (bvh_tail_levels() > 1 ? tail_stride(1, frames, bvh_tail_lanes()) : 0));
     if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
     if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
     return b;
@@ -1819,6 +1987,19 @@ int ensure_frames(int frames) {
         RC(dalloc(&gp->queue.B, qn));
         RC(dalloc(&gp->queue.C, qn));
         RC(dalloc(&gp->queue.D, qn));
+        gp->tail_lanes = bvh_tail_lanes();
+        gp->tail_levels = bvh_tail_levels();
+        if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
+            gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
+            for (int k = 0; k < std::min(2, gp->tail_levels); ++k) {   // one level: one buffer
+                TailBuf& t = gp->tail[k];
+                t.stride = tail_stride(k, frames, gp->tail_lanes);
+                t.cap = t.stride * NSEG;
+                RC(dalloc(&t.node, (size_t)t.cap));
+                RC(dalloc(&t.hit, (size_t)t.cap));
+                RC(dalloc(&t.stack, (size_t)t.cap * gp->tail_depth));
+            }
+        }
     }
     if (frames > 1) RC(dalloc(&gp->d_contrib, (size_t)gp->pixels_total * 3 * frames));
     gp->sc.contrib = gp->d_contrib;
@@ -3549,7 +3730,8 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, rec[i].start, rec[i].stop);
                 int k = rec[i].kind;
-                if (k >= 300) { tail_ms += ms; tail_from = k - 300; }
+                if (k >= 400) { bounce_ms[k - 400] += ms; bvh_ms[k - 400] += ms; }   // k_bvh_tail
+                else if (k >= 300) { tail_ms += ms; tail_from = k - 300; }
                 else if (k >= 200) { bounce_ms[k - 200] += ms; bvh_ms[k - 200] += ms; }
                 else if (k >= 100) bounce_ms[k - 100] += ms;
                 else if (k == 0) cam_ms += ms;

@@ -388,9 +388,11 @@ class PathTracer:
 
     def section_counters(self, reset: bool = True) -> dict:
         """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""
-        buf = (ctypes.c_uint64 * 24)()
-        _check(lib.pt_debug_section_counters(buf, 24, int(reset)), "pt_debug_section_counters")
-        return {k: int(buf[i]) for i, k in enumerate(self.SECTIONS)}
+        buf = (ctypes.c_uint64 * 40)()
+        _check(lib.pt_debug_section_counters(buf, 40, int(reset)), "pt_debug_section_counters")
+        out = {k: int(buf[i]) for i, k in enumerate(self.SECTIONS)}
+        out["bvh_lanes_hist"] = [int(buf[len(self.SECTIONS) + i]) for i in range(16)]
+        return out
 
     # ---- single-kernel entry points (tests) ----
     def test_camera(self, iteration: int) -> np.ndarray:

@@ -52,6 +52,21 @@ print(json.dumps({'copy_first': os.environ.get('PT_SPEC_COPY_FIRST'), **bench.ap
         benchapi) step bench_api 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-spread ;;
         trim) for r in 1 2 3; do for t in 0 120; do PT_GRID_TRIM_PCT=$t step trim_${t}_$r 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-api --no-spread; done; done
             grep -h '^{' gpurun_out/trim_*.log | python -c "import sys,json; [print(json.loads(l)['ms_per_step']) for l in sys.stdin]" ;;
+        hist) step sec_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_bunny.json
+            step sec_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana.json ;;
+        tailtest) step pytest_tail 400 $PYT tests/test_bvh_tail.py -m gpu ;;
+        mesh16) PT_BVH_TAIL_LANES=${MESH_TAIL:-16} step pytest_mesh16 600 $PYT tests/test_gpu_parity.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or config5 or speculated" ;;
+        tailab) AB_TAG=tail_bunny AB_ENVS="$(for a in ${TAIL_ARMS:-0 4 8 16}; do printf "PT_BVH_TAIL_LANES=%s " $a; done)" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_tail_bunny 900 bash tools/ab_env.sh
+            AB_TAG=tail_khaslana AB_ENVS="$(for a in ${TAIL_ARMS:-0 4 8 16}; do printf "PT_BVH_TAIL_LANES=%s " $a; done)" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_tail_khaslana 900 bash tools/ab_env.sh ;;
+        levelab) ARMS="PT_BVH_TAIL_LANES=0 PT_BVH_TAIL_LEVELS=1 PT_BVH_TAIL_LEVELS=2 PT_BVH_TAIL_LEVELS=3 PT_BVH_TAIL_LEVELS=2,PT_BVH_TAIL_LANES=24"
+            AB_TAG=lvl_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lvl_bunny 900 bash tools/ab_env.sh
+            AB_TAG=lvl_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_lvl_khaslana 900 bash tools/ab_env.sh ;;
+        gridab) ARMS="${GRID_ARMS:-PT_BVH_TAIL_CHUNKS=100000 PT_BVH_TAIL_CHUNKS=64 PT_BVH_TAIL_CHUNKS=128 PT_BVH_TAIL_CHUNKS=256 PT_BVH_TAIL_CHUNKS=128,PT_BVH_TAIL_LEVELS=1 PT_BVH_TAIL_LANES=0}"
+            AB_TAG=grid_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_grid_bunny 900 bash tools/ab_env.sh
+            AB_TAG=grid_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_grid_khaslana 900 bash tools/ab_env.sh ;;
+        meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
+            step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
+            step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -55,6 +55,16 @@ def main():
            "bvh_wave_iters_per_wave": round(c["n_bvh_witers"] / max(1, c["n_waves"]), 2),
            "bvh_simt_efficiency": round(c["n_nodes"] / max(1, 64 * c["n_bvh_witers"]), 3),
            "aabb_decision_mismatches": c["n_aabb_mismatch"], "raw": c}
+    # k_bvh_bounce wave steps by active lanes (bins of 4): the steps a wave takes below a given
+    # occupancy, and the lane-steps they do (bin centres)
+    h = c["bvh_lanes_hist"]
+    wt = max(1, sum(h))
+    out["bvh_steps_by_active_lanes"] = {
+        "bins_of_4": h,
+        "share_of_wave_steps_below": {str(4 * k): round(sum(h[:k]) / wt, 4) for k in (2, 4, 8)},
+        "share_of_lane_steps_below": {str(4 * k): round(sum(h[i] * (4 * i + 2.5) for i in range(k)) /
+                                                        max(1, sum(h[i] * (4 * i + 2.5) for i in range(16))), 4)
+                                      for k in (2, 4, 8)}}
     out["skip_camera"] = os.environ.get("PT_SECTIONS_SKIP_CAMERA") is not None
     print(json.dumps(out, indent=1))
     if args.out:
