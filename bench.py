@@ -485,8 +485,9 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
         else:
             nbytes += 4 * n_in + 2 * STATE_BYTES * n_out
     if pipeline == "fused" and any(prof["bvh_ms"][:depth]):
-        name = ("k_bounce + k_bvh_bounce + k_bvh_tail (fused bounce; mesh rays traversed and shaded by the "
-                "second kernel, the last rays of its waves by the third), one set of launches per bounce per pass")
+        name = ("k_bounce + k_bvh_bounce + k_bvh_tail_trav + k_bvh_tail_shade (fused bounce; mesh rays "
+                "traversed and shaded by the second kernel, the last rays of its waves by the third and fourth), "
+                "one set of launches per bounce per pass")
     elif pipeline == "fused":
         name = "k_bounce (fused camera|intersect|shade|gather|compact, one launch per bounce per pass)"
     else:
@@ -501,7 +502,8 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
     if traffic_file:
         # a config with its own committed PMC digest (profiles/rNN_traffic_<tag>.json): both
         # kernels of a bounce, bytes per frame scaled to this run's frames per launch pair
-        keys = ("k_bounce", "k_bvh_bounce", "k_bvh_tail") if pipeline == "fused" else ("k_compact_scatter",)
+        keys = (("k_bounce", "k_bvh_bounce", "k_bvh_tail_trav", "k_bvh_tail_shade") if pipeline == "fused"
+                else ("k_compact_scatter",))
         per_frame = sum(v.get("hbm_bytes_per_frame", 0) for k, v in _pmc_digest(traffic_file).items() if k in keys)
         traffic = int(per_frame * steps / launches) if per_frame else None
     line = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -279,8 +279,10 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
  * triangles, [13] traversed rays, [14] box-decision mismatches (node-array traversal), [15] wave
  * traversal iterations, [16] leaf visits, [17] traversed rays whose mesh hit wins, [18] node
  * visits of the rays whose mesh hit does not win, [19] rays culled at the root, [20..35] wave
- * traversal iterations by active lanes in bins of 4 (1-4, 5-8, ..); n <= 40.  `reset` zeroes
- * them after the read. */
+ * traversal iterations by active lanes in bins of 4 (1-4, 5-8, ..), [36..51] the same for the
+ * handed-over traversals' kernel, [52..67] handed-over rays by stack depth (8 buckets: count,
+ * nodes visited after), [68..71] by a hit found before (no: count, nodes; yes: count, nodes);
+ * n <= 76.  `reset` zeroes them after the read. */
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset);
 
 #ifdef __cplusplus

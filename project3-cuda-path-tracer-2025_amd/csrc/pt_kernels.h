@@ -119,8 +119,12 @@ enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EX
        SEC_N_WAVES, SEC_N_LANES, SEC_N_NODES, SEC_N_TRIS, SEC_N_BVH_RAYS, SEC_N_BVH_ITERS, SEC_N_BVH_WITERS,
        SEC_N_LEAVES, SEC_N_BVH_HITS, SEC_N_MISS_NODES, SEC_N_ROOT_CULLED,
        SEC_BVH_LANES_HIST,                    // 16 bins: wave traversal steps by active lanes (1-4, 5-8, ..)
-       SEC_COUNT = SEC_BVH_LANES_HIST + 16 };
-constexpr int SEC_SLOTS = 40;
+       SEC_TAIL_LANES_HIST = SEC_BVH_LANES_HIST + 16,   // the same for k_bvh_tail_trav's steps
+       SEC_TAIL_BY_SP = SEC_TAIL_LANES_HIST + 16,   // handed-over rays by stack depth at the hand-over
+                                                    // (0, 1, 2, 3, 4-5, 6-7, 8-11, 12+): count, nodes after
+       SEC_TAIL_BY_HIT = SEC_TAIL_BY_SP + 16,       // ... by "a hit found before": no (count, nodes), yes
+       SEC_COUNT = SEC_TAIL_BY_HIT + 4 };
+constexpr int SEC_SLOTS = 76;
 __device__ unsigned long long g_sections[SEC_SLOTS];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
 PT_DEV void sec_add(int k, uint64_t v) {
@@ -586,7 +590,7 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
     return st.t_hit;
 }
 
-// A ray's traversal handed from one wave to another (k_bvh_bounce -> k_bvh_tail): the best hit so
+// A ray's traversal handed from one wave to another (k_bvh_bounce -> k_bvh_tail_trav): the best hit so
 // far, the node to expand next and the stack.  The culls' thresholds ride in the stack entries and
 // the ray's reciprocals, exactness and the wave's fast-box flag are recomputed; which box routine
 // a wave uses never changes a decision, so the resumed traversal visits what the ray would have.
@@ -606,16 +610,17 @@ PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node) {
 }
 // expand nodes until the ray is finished (st.cur < 0) or -- defer > 0 -- until no more than
 // `defer` lanes of the wave are still traversing: those stop with st.cur >= 0 (wave steps with a
-// handful of lanes cost a wave slot each for a few lanes of work; k_bvh_tail resumes them 64 to a
-// wave).  Counters (COUNT) as bvh_intersect_pairs', the per-ray ones left to the caller.
+// handful of lanes cost a wave slot each for a few lanes of work; k_bvh_tail_trav resumes them in
+// full waves).  Counters (COUNT) as bvh_intersect_pairs', the per-ray ones left to the caller.
 template <bool COUNT = false>
-PT_DEV void trav_run(const SceneDev& sc, TravState& st, int* stack, int defer, int& n_nodes, int& n_tris) {
+PT_DEV void trav_run(const SceneDev& sc, TravState& st, int* stack, int defer, int& n_nodes, int& n_tris,
+                     int hist = SEC_BVH_LANES_HIST) {
     while (st.cur >= 0) {
         const int lanes = __popcll(__builtin_amdgcn_read_exec());   // wave-uniform
         if (lanes <= defer) break;
         if (COUNT) {
             sec_add(SEC_N_BVH_WITERS, 1);
-            sec_add(SEC_BVH_LANES_HIST + (lanes - 1) / 4, 1);
+            sec_add(hist + (lanes - 1) / 4, 1);
         }
         trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
     }

@@ -65,8 +65,7 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
     for (int i = t; i < rows * NSEG; i += blockDim.x) (&ctl->cnt[0][0][0])[i * CNT_PAD] = 0;
     for (int i = t; i < rows * NSEG; i += blockDim.x) {
         (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
-#pragma unroll
-        for (int l = 1; l <= 4; ++l) (&ctl->qcnt[0][0][0])[i * CNT_PAD + l] = 0;   // handed-over traversals
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD + 1] = 0;   // handed-over traversals
     }
     __syncthreads();
     if (t == 0) {
@@ -228,12 +227,11 @@ struct QueueBuf {
     float4 *A, *B, *C, *D;   // D = t_min | seed.xyz
     int stride;              // entries per queue segment (segment s at s * stride, FrameCtl::qcnt)
 };
-// Traversals handed from k_bvh_bounce to k_bvh_tail (see trav_run), and from one k_bvh_tail level
-// to the next: per entry the queue slot and the saved node (trav_saved_node), the best hit so far,
-// and the stack (entry i of e at stack[i * cap + e]).  Segment s (at s * stride; counter
-// FrameCtl::qcnt[b][s][level]) holds the rays of the previous kernel's blocks of segment s, so
-// k_bvh_tail's survivors fit where theirs would have.  Two buffers, levels alternating.
-constexpr int MAX_TAIL_LEVELS = 4;
+// Traversals handed from k_bvh_bounce to k_bvh_tail_trav (see trav_run): per entry the queue slot
+// and the saved node (trav_saved_node), the best hit so far (the final hit once k_bvh_tail_trav is
+// done), and the stack (entry i of e at stack[i * cap + e]).  Segment s (at s * stride; counter
+// FrameCtl::qcnt[b][s][1]) holds the rays of k_bvh_bounce's blocks of segment s, so
+// k_bvh_tail_shade's survivors fit where theirs would have.
 struct TailBuf {
     int2* node;     // queue slot | trav_saved_node
     float4* hit;    // trav_saved_hit
@@ -530,7 +528,7 @@ __global__ __launch_bounds__(BLOCK) void k_tail(SceneDev sc, PathBuf in, FrameCt
 #endif
 
 // after the traversal: the path's other words, the hit, shading (the shared end of k_bvh_bounce
-// and k_bvh_tail)
+// and k_bvh_tail_shade)
 template <int VAR>
 PT_DEV void bvh_finish_path(const SceneDev& sc, const QueueBuf& q, int qs, int iter, PathReg& p, const TravState& st) {
     float u = 0.f, v = 0.f;
@@ -558,7 +556,7 @@ PT_DEV void bvh_count_ray(const TravState& st, float t_prim, int n_nodes) {
     }
 }
 
-// hand the calling lanes' traversals (st.cur >= 0) over to the next level: one atomic per wave.
+// hand the calling lanes' traversals (st.cur >= 0) over to k_bvh_tail_trav: one atomic per wave.
 // false: the segment is full at this lane's slot -- the caller finishes it itself.  The counter
 // still counts it; every slot below min(counter, stride) is written by the lane that reserved it.
 PT_DEV bool tail_put(const TailBuf& t, int* ctr, int seg, int qs, const TravState& st, const int* s_stack) {
@@ -610,10 +608,14 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
         TravState st;
         trav_begin(sc, st, p.o, p.d, t_prim);
         if (CNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
-        trav_run<CNT>(sc, st, s_stack + tid, defer, n_nodes, n_tris);
-        if (st.cur >= 0) {   // handed over: the wave's last few traversals go on 64 to a wave
-            handed = tail_put(tail, &ctl->qcnt[bounce][seg][1], seg, qs, st, s_stack + tid);
-            if (!handed) trav_run<CNT>(sc, st, s_stack + tid, 0, n_nodes, n_tris);   // no room: finish here
+        // handed over: the wave's last few traversals go on 64 to a wave (no room: finish here)
+        for (int d = defer;; d = 0) {
+            trav_run<CNT>(sc, st, s_stack + tid, d, n_nodes, n_tris);
+            if (st.cur < 0) break;
+            if (tail_put(tail, &ctl->qcnt[bounce][seg][1], seg, qs, st, s_stack + tid)) {
+                handed = true;
+                break;
+            }
         }
         if (CNT) {
             sec_add_lanes(SEC_N_NODES, n_nodes);
@@ -631,55 +633,108 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
     if (surv) store_path(out, seg * seg_stride + si, p);
 }
 
-// The traversals handed over to `level` (by k_bvh_bounce, or by the previous level), resumed 64
-// to a wave and finished like k_bvh_bounce's own -- or, defer > 0, handed on to level + 1 the same
-// way.  Block (j, s) = blockIdx (j * NSEG + s) takes entries j * BLOCK .. of segment s of `tin`,
-// and its survivors go to output segment s, with those of the blocks the rays came from.
+// The handed-over traversals, run by a fixed grid of waves that refill their lanes as rays
+// finish.  Wave w of segment s takes the entries [w * per, (w + 1) * per) of the
+// segment (per >= 64, from the segment's count: no atomics); whenever `refill` or more lanes are
+// idle it loads the next entries into them, so a wave drains once per range instead of once per
+// 64 rays.  Traversal only: a finished ray's result (t, u, v, triangle) replaces its saved hit,
+// and k_bvh_tail_shade shades the entries in full waves.  No barrier: waves leave on their own.
 template <int VAR>
-__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail(SceneDev sc, QueueBuf q, TailBuf tin, TailBuf tout,
-                                                               int level, int defer, PathBuf out, FrameCtl* ctl,
-                                                               float* __restrict__ image, int bounce, int seg_stride) {
+__global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc, QueueBuf q, TailBuf t, FrameCtl* ctl,
+                                                                    int bounce, int refill, int min_range) {
     extern __shared__ float4 s_dyn[];
+    int* s_stack = reinterpret_cast<int*>(s_dyn) + threadIdx.x;
     const int seg = blockIdx.x & (NSEG - 1);
-    const int n = min(ctl->qcnt[bounce][seg][level], tin.stride);   // the counter counts refused lanes too
+    const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
+    const int waves = (gridDim.x / NSEG) * (BLOCK / 64);
+    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / NSEG) * (BLOCK / 64) + (int)(threadIdx.x >> 6));
+    const int used = max(1, min(waves, (n + min_range - 1) / min_range));
+    const int per = (n + used - 1) / used;
+    int next = w * per;
+    const int hi = min(n, next + per);
+    if (w >= used || next >= hi) return;   // wave-uniform
+    constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
+    int e = -1, qs = 0, n_nodes = 0, n_tris = 0, sp0 = 0;
+    bool hit0 = false;
+    TravState st;
+    st.cur = -1;
+    while (true) {
+        const uint64_t idle = __ballot(e < 0);
+        const int n_idle = __popcll(idle);
+        if (next < hi && (n_idle >= refill || n_idle == 64)) {
+            if (e < 0) {
+                const int k = next + mbcnt(idle);
+                if (k < hi) {
+                    e = seg * t.stride + k;
+                    const int2 nd = t.node[e];
+                    qs = nd.x;
+                    const float4 a = q.A[qs], b = q.B[qs];
+                    trav_resume(st, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), t.hit[e], nd.y);
+                    for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK] = t.stack[(size_t)i * t.cap + e];
+                    n_nodes = n_tris = 0;
+                    if (CNT) {
+                        sp0 = st.sp;
+                        hit0 = st.btri != 0x7fffffff;
+                    }
+                }
+            }
+            next += n_idle;
+        }
+        const int lanes = __popcll(__ballot(e >= 0));
+        if (lanes == 0) break;   // nothing left in the range
+        if (e >= 0) {
+            if (CNT) {
+                sec_add(SEC_N_BVH_WITERS, 1);
+                sec_add(SEC_TAIL_LANES_HIST + (lanes - 1) / 4, 1);
+            }
+            trav_step<CNT>(sc, st, s_stack, n_nodes, n_tris);
+            if (st.cur < 0) {
+                t.hit[e] = trav_saved_hit(st);
+                if (CNT) {
+                    sec_add_lanes(SEC_N_NODES, n_nodes);
+                    sec_add_lanes(SEC_N_TRIS, n_tris);
+                    bvh_count_ray<CNT>(st, q.D[qs].x, n_nodes);
+                    const int bk = sp0 < 4 ? sp0 : sp0 < 6 ? 4 : sp0 < 8 ? 5 : sp0 < 12 ? 6 : 7;
+                    sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk, 1);
+                    sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk + 1, n_nodes);
+                    sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 2 : 0), 1);
+                    sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 3 : 1), n_nodes);
+                }
+                e = -1;
+            }
+        }
+    }
+}
+// ... and their shading, gather and compaction, as k_bvh_bounce's (block (j, s) = blockIdx
+// (j * NSEG + s): entries j * BLOCK .. of segment s, survivors to output segment s)
+template <int VAR>
+__global__ __launch_bounds__(BLOCK) void k_bvh_tail_shade(SceneDev sc, QueueBuf q, TailBuf t, PathBuf out, FrameCtl* ctl,
+                                                          float* __restrict__ image, int bounce, int seg_stride) {
+    const int seg = blockIdx.x & (NSEG - 1);
+    const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
     const int block_start = (blockIdx.x / NSEG) * BLOCK;
     if (block_start >= n) return;
-    int* s_stack = reinterpret_cast<int*>(s_dyn);
     const int iter = ctl->iter;
     const bool to_plane = ctl->batch > 1 || ctl->plane != 0;
     const int tid = threadIdx.x;
     const bool active = block_start + tid < n;
-    bool handed = false;
     PathReg p;
     p.rb = 0;
     if (active) {
-        const int e = seg * tin.stride + block_start + tid;
-        const int2 nd = tin.node[e];
-        const int qs = nd.x;
-        const float4 a = q.A[qs], b = q.B[qs];
+        const int e = seg * t.stride + block_start + tid;
+        const int qs = t.node[e].x;
+        const float4 a = q.A[qs], b = q.B[qs], h = t.hit[e];
         p.o = mk(a.x, a.y, a.z);
         p.d = mk(b.x, b.y, b.z);
         TravState st;
-        trav_resume(st, p.o, p.d, tin.hit[e], nd.y);
-        for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK + tid] = tin.stack[(size_t)i * tin.cap + e];
-        constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
-        int n_nodes = 0, n_tris = 0;
-        trav_run<CNT>(sc, st, s_stack + tid, defer, n_nodes, n_tris);
-        if (st.cur >= 0) {
-            handed = tail_put(tout, &ctl->qcnt[bounce][seg][level + 1], seg, qs, st, s_stack + tid);
-            if (!handed) trav_run<CNT>(sc, st, s_stack + tid, 0, n_nodes, n_tris);   // no room: finish here
-        }
-        if (CNT) {
-            sec_add_lanes(SEC_N_NODES, n_nodes);
-            sec_add_lanes(SEC_N_TRIS, n_tris);
-        }
-        if (!handed) {
-            bvh_count_ray<CNT>(st, q.D[qs].x, n_nodes);
-            bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
-        }
+        st.t_hit = h.x;
+        st.bu = h.y;
+        st.bv = h.z;
+        st.btri = __float_as_int(h.w);
+        bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
     }
-    const bool surv = active && !handed && p.rb > 0;
-    if (active && !handed && !surv) gather_into_image(image, sc, to_plane, p);
+    const bool surv = active && p.rb > 0;
+    if (active && !surv) gather_into_image(image, sc, to_plane, p);
     int si, unused;
     block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
     if (surv) store_path(out, seg * seg_stride + si, p);
@@ -1110,8 +1165,9 @@ struct State {
     bool split = false;              // VAR_BVH_SPLIT active (fused, fast BVH on the pair layout)
     bool no_tex = false;             // no textured / bump-mapped material (VAR_NO_TEX kernels)
     QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
-    TailBuf tail[2] = {};            // the traversals k_bvh_bounce hands to k_bvh_tail (levels alternate)
-    int tail_lanes = 0, tail_levels = 0;   // bvh_tail_lanes(), bvh_tail_levels()
+    TailBuf tail{};                  // the traversals k_bvh_bounce hands to k_bvh_tail_trav
+    int tail_lanes = 0;              // bvh_tail_lanes()
+    int tail_refill = 16, tail_trav_blocks = 224, tail_min_range = 64;   // PT_BVH_TAIL_REFILL / _TRAV_BLOCKS / _MIN_RANGE
     int tail_depth = 0;              // stack entries per handed-over traversal
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
@@ -1255,14 +1311,13 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
         const size_t stack_bytes = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int);
         // the handed-over stacks were sized for the pair tree of the allocation (ensure_frames)
         if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
-        const int levels = gp->tail_lanes > 0 ? gp->tail_levels : 0;
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail[0],
-               levels > 0 ? gp->tail_lanes : 0, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
-        for (int l = 1; l <= levels; ++l) {
-            const TailBuf& tin = gp->tail[(l - 1) & 1];
-            launch(400 + b, k_bvh_tail<VAR>, dim3(NSEG * nblocks(tin.stride)), dim3(BLOCK), stack_bytes, gp->sc,
-                   gp->queue, tin, gp->tail[l & 1], l, l < levels ? gp->tail_lanes : 0, out, gp->d_ctl, gp->d_image, b,
-                   gp->seg_stride);
+        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail,
+               gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
+        if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
+            launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
+                   gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill, gp->tail_min_range);
+            launch(400 + b, k_bvh_tail_shade<VAR>, dim3(NSEG * nblocks(gp->tail.stride)), dim3(BLOCK), 0, gp->sc,
+                   gp->queue, gp->tail, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
         }
     }
 }
@@ -1898,12 +1953,10 @@ void free_pass_buffers() {
     dfree(gp->queue.B);
     dfree(gp->queue.C);
     dfree(gp->queue.D);
-    for (TailBuf& t : gp->tail) {
-        dfree(t.node);
-        dfree(t.hit);
-        dfree(t.stack);
-        t.stride = t.cap = 0;
-    }
+    dfree(gp->tail.node);
+    dfree(gp->tail.hit);
+    dfree(gp->tail.stack);
+    gp->tail.stride = gp->tail.cap = 0;
     dfree(gp->d_contrib);
     gp->sc.contrib = nullptr;
     gp->alloc_frames = 0;
@@ -1922,28 +1975,20 @@ int q_stride_for(int frames) {
     const int nb = nblocks(std::max(1, gp->local_pixels * frames));
     return ((nb + NSEG - 1) / NSEG) * BLOCK;
 }
-// k_bvh_bounce hands a wave's traversals to k_bvh_tail once no more than this many of its lanes
-// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 32)
+// k_bvh_bounce hands a wave's traversals to k_bvh_tail_trav once no more than this many of its lanes
+// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56)
 int bvh_tail_lanes() {
     const char* e = getenv("PT_BVH_TAIL_LANES");
-    return std::min(32, std::max(0, e ? atoi(e) : 16));
+    return std::min(56, std::max(0, e ? atoi(e) : 24));
 }
-// ... in up to this many k_bvh_tail levels, the last one finishing every traversal
-// (PT_BVH_TAIL_LEVELS, 1 .. MAX_TAIL_LEVELS)
-int bvh_tail_levels() {
-    const char* e = getenv("PT_BVH_TAIL_LEVELS");
-    return std::min(MAX_TAIL_LEVELS, std::max(1, e ? atoi(e) : 1));
-}
-// entries per segment of tail buffer k: what the kernel filling it can hand over -- `lanes` per
-// wave of its blocks of one segment (k_bvh_bounce: buffer 0; a level reading buffer 0: buffer 1;
-// the levels after that shrink).  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane
-// that finds its segment full then finishes its ray itself (tail_put).  A cap measured slower at
-// every size tried: bunny's passes hand over ~10 % of 128 frames' rays (DESIGN Appendix A).
-int tail_stride(int k, int frames, int lanes) {
+// entries per tail segment: what k_bvh_bounce can hand over, `lanes` per wave of its blocks of one
+// segment.  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane that finds its segment
+// full then finishes its ray itself (tail_put).  A cap measured slower at every size tried:
+// bunny's passes hand over ~20 % of 128 frames' queued rays (DESIGN Appendix A).
+int tail_stride(int frames, int lanes) {
     const char* e = getenv("PT_BVH_TAIL_CHUNKS");
     const int nb = nblocks(std::max(1, gp->local_pixels * frames));
-    const int s0 = ((nb + NSEG - 1) / NSEG) * (BLOCK / 64) * lanes;
-    const int s = k == 0 ? s0 : nblocks(s0) * (BLOCK / 64) * lanes;
+    const int s = ((nb + NSEG - 1) / NSEG) * (BLOCK / 64) * lanes;
     return e && atoi(e) > 0 ? std::min(s, atoi(e) * BLOCK) : s;
 }
 // paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
@@ -1958,8 +2003,7 @@ size_t pass_bytes(int frames, bool staged) {
     if (gp->split) b += 4 * sizeof(float4) * (size_t)q_stride_for(frames) * NSEG;   // traversal queue
     if (gp->split && bvh_tail_lanes() > 0)   // handed-over traversals
         b += (sizeof(int2) + sizeof(float4) + sizeof(int) * std::max(1, gp->sc.pair_stack_depth)) * NSEG *
-             (size_t)(tail_stride(0, frames, bvh_tail_lanes()) +
-                      (bvh_tail_levels() > 1 ? tail_stride(1, frames, bvh_tail_lanes()) : 0));
+             (size_t)tail_stride(frames, bvh_tail_lanes());
     if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
     if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
     return b;
@@ -1988,17 +2032,17 @@ int ensure_frames(int frames) {
         RC(dalloc(&gp->queue.C, qn));
         RC(dalloc(&gp->queue.D, qn));
         gp->tail_lanes = bvh_tail_lanes();
-        gp->tail_levels = bvh_tail_levels();
+        gp->tail_refill = getenv("PT_BVH_TAIL_REFILL") ? std::max(1, std::min(64, atoi(getenv("PT_BVH_TAIL_REFILL")))) : 16;
+        gp->tail_trav_blocks = getenv("PT_BVH_TAIL_TRAV_BLOCKS") ? std::max(1, atoi(getenv("PT_BVH_TAIL_TRAV_BLOCKS"))) : 224;
+        gp->tail_min_range = getenv("PT_BVH_TAIL_MIN_RANGE") ? std::max(64, atoi(getenv("PT_BVH_TAIL_MIN_RANGE"))) : 64;
         if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
             gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
-            for (int k = 0; k < std::min(2, gp->tail_levels); ++k) {   // one level: one buffer
-                TailBuf& t = gp->tail[k];
-                t.stride = tail_stride(k, frames, gp->tail_lanes);
-                t.cap = t.stride * NSEG;
-                RC(dalloc(&t.node, (size_t)t.cap));
-                RC(dalloc(&t.hit, (size_t)t.cap));
-                RC(dalloc(&t.stack, (size_t)t.cap * gp->tail_depth));
-            }
+            TailBuf& t = gp->tail;
+            t.stride = tail_stride(frames, gp->tail_lanes);
+            t.cap = t.stride * NSEG;
+            RC(dalloc(&t.node, (size_t)t.cap));
+            RC(dalloc(&t.hit, (size_t)t.cap));
+            RC(dalloc(&t.stack, (size_t)t.cap * gp->tail_depth));
         }
     }
     if (frames > 1) RC(dalloc(&gp->d_contrib, (size_t)gp->pixels_total * 3 * frames));
@@ -3730,7 +3774,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, rec[i].start, rec[i].stop);
                 int k = rec[i].kind;
-                if (k >= 400) { bounce_ms[k - 400] += ms; bvh_ms[k - 400] += ms; }   // k_bvh_tail
+                if (k >= 400) { bounce_ms[k - 400] += ms; bvh_ms[k - 400] += ms; }   // k_bvh_tail_trav / _shade
                 else if (k >= 300) { tail_ms += ms; tail_from = k - 300; }
                 else if (k >= 200) { bounce_ms[k - 200] += ms; bvh_ms[k - 200] += ms; }
                 else if (k >= 100) bounce_ms[k - 100] += ms;

@@ -388,10 +388,13 @@ class PathTracer:
 
     def section_counters(self, reset: bool = True) -> dict:
         """Fused-kernel section counters (variant bit 4); see pathtrace_abi.h."""
-        buf = (ctypes.c_uint64 * 40)()
-        _check(lib.pt_debug_section_counters(buf, 40, int(reset)), "pt_debug_section_counters")
+        buf = (ctypes.c_uint64 * 76)()
+        _check(lib.pt_debug_section_counters(buf, 76, int(reset)), "pt_debug_section_counters")
         out = {k: int(buf[i]) for i, k in enumerate(self.SECTIONS)}
         out["bvh_lanes_hist"] = [int(buf[len(self.SECTIONS) + i]) for i in range(16)]
+        out["tail_lanes_hist"] = [int(buf[len(self.SECTIONS) + 16 + i]) for i in range(16)]
+        out["tail_by_sp"] = [int(buf[len(self.SECTIONS) + 32 + i]) for i in range(16)]
+        out["tail_by_hit"] = [int(buf[len(self.SECTIONS) + 48 + i]) for i in range(4)]
         return out
 
     # ---- single-kernel entry points (tests) ----

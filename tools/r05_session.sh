@@ -37,33 +37,18 @@ for s in "$@"; do
             [ -z "${AB_SKIP_CORNELL:-}" ] && AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
             AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
             AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
-        secq16)
-            PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/q16.so step sec_q16_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_q16_bunny.json
-            PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/q16.so step sec_q16_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_q16_khaslana.json ;;
         profiles) step profiles 1100 bash tools/r05_profiles.sh ;;
         apicopy)
             step prof_api_copy 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/prof_api_copy -o run --output-format csv -- python tools/api_trace.py run copy
             python tools/api_trace.py overlap gpurun_out/prof_api_copy/run_kernel_trace.csv gpurun_out/prof_api_copy/run_memory_copy_trace.csv --out gpurun_out/api_copy_overlap.json ;;
-        apiab) for r in 1 2; do for m in 0 1; do PT_SPEC_COPY_FIRST=$m step api_ab_${m}_$r 200 python -c "
-import sys, json; sys.argv=['bench.py']; import bench, os
-sys.path.insert(0, bench.PKG); import ptamd
-tr = ptamd.PathTracer(ptamd.SceneFile(bench.SCENE)); tr.trace_frames(1, 5); tr.synchronize()
-print(json.dumps({'copy_first': os.environ.get('PT_SPEC_COPY_FIRST'), **bench.api_frame_ms(tr, 100)}))" ; done; done ;;
         benchapi) step bench_api 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-spread ;;
-        trim) for r in 1 2 3; do for t in 0 120; do PT_GRID_TRIM_PCT=$t step trim_${t}_$r 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-api --no-spread; done; done
-            grep -h '^{' gpurun_out/trim_*.log | python -c "import sys,json; [print(json.loads(l)['ms_per_step']) for l in sys.stdin]" ;;
         hist) step sec_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_bunny.json
             step sec_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana.json ;;
         tailtest) step pytest_tail 400 $PYT tests/test_bvh_tail.py -m gpu ;;
-        mesh16) PT_BVH_TAIL_LANES=${MESH_TAIL:-16} step pytest_mesh16 600 $PYT tests/test_gpu_parity.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or config5 or speculated" ;;
-        tailab) AB_TAG=tail_bunny AB_ENVS="$(for a in ${TAIL_ARMS:-0 4 8 16}; do printf "PT_BVH_TAIL_LANES=%s " $a; done)" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_tail_bunny 900 bash tools/ab_env.sh
-            AB_TAG=tail_khaslana AB_ENVS="$(for a in ${TAIL_ARMS:-0 4 8 16}; do printf "PT_BVH_TAIL_LANES=%s " $a; done)" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_tail_khaslana 900 bash tools/ab_env.sh ;;
-        levelab) ARMS="PT_BVH_TAIL_LANES=0 PT_BVH_TAIL_LEVELS=1 PT_BVH_TAIL_LEVELS=2 PT_BVH_TAIL_LEVELS=3 PT_BVH_TAIL_LEVELS=2,PT_BVH_TAIL_LANES=24"
-            AB_TAG=lvl_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lvl_bunny 900 bash tools/ab_env.sh
-            AB_TAG=lvl_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_lvl_khaslana 900 bash tools/ab_env.sh ;;
-        gridab) ARMS="${GRID_ARMS:-PT_BVH_TAIL_CHUNKS=100000 PT_BVH_TAIL_CHUNKS=64 PT_BVH_TAIL_CHUNKS=128 PT_BVH_TAIL_CHUNKS=256 PT_BVH_TAIL_CHUNKS=128,PT_BVH_TAIL_LEVELS=1 PT_BVH_TAIL_LANES=0}"
-            AB_TAG=grid_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_grid_bunny 900 bash tools/ab_env.sh
-            AB_TAG=grid_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_grid_khaslana 900 bash tools/ab_env.sh ;;
+        meshlanes) PT_BVH_TAIL_LANES=${MESH_TAIL:-16} step pytest_meshlanes 600 $PYT tests/test_gpu_parity.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or config5 or speculated" ;;
+        laneab) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=0 PT_BVH_TAIL_LANES=16 PT_BVH_TAIL_LANES=24 PT_BVH_TAIL_LANES=32}"
+            AB_TAG=lane_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lane_bunny 900 bash tools/ab_env.sh
+            AB_TAG=lane_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_lane_khaslana 900 bash tools/ab_env.sh ;;
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;

@@ -57,14 +57,24 @@ def main():
            "aabb_decision_mismatches": c["n_aabb_mismatch"], "raw": c}
     # k_bvh_bounce wave steps by active lanes (bins of 4): the steps a wave takes below a given
     # occupancy, and the lane-steps they do (bin centres)
-    h = c["bvh_lanes_hist"]
-    wt = max(1, sum(h))
-    out["bvh_steps_by_active_lanes"] = {
-        "bins_of_4": h,
-        "share_of_wave_steps_below": {str(4 * k): round(sum(h[:k]) / wt, 4) for k in (2, 4, 8)},
-        "share_of_lane_steps_below": {str(4 * k): round(sum(h[i] * (4 * i + 2.5) for i in range(k)) /
-                                                        max(1, sum(h[i] * (4 * i + 2.5) for i in range(16))), 4)
-                                      for k in (2, 4, 8)}}
+    for key, name in (("bvh_lanes_hist", "bvh_steps_by_active_lanes"), ("tail_lanes_hist", "tail_steps_by_active_lanes")):
+        h = c[key]
+        wt = max(1, sum(h))
+        lane_steps = sum(h[i] * (4 * i + 2.5) for i in range(16))
+        out[name] = {
+            "bins_of_4": h,
+            "wave_steps": sum(h),
+            "simt_efficiency_est": round(lane_steps / (64 * wt), 3),
+            "share_of_wave_steps_below": {str(4 * k): round(sum(h[:k]) / wt, 4) for k in (2, 4, 8)},
+            "share_of_lane_steps_below": {str(4 * k): round(sum(h[i] * (4 * i + 2.5) for i in range(k)) /
+                                                            max(1, lane_steps), 4) for k in (2, 4, 8)}}
+    # handed-over rays: how many, and the nodes they still visit, by stack depth and by whether a
+    # hit was found before the hand-over
+    bs, bh = c["tail_by_sp"], c["tail_by_hit"]
+    out["tail_rays_by_stack_depth"] = {lab: {"rays": bs[2 * k], "nodes_per_ray": round(bs[2 * k + 1] / max(1, bs[2 * k]), 2)}
+                                       for k, lab in enumerate(["0", "1", "2", "3", "4-5", "6-7", "8-11", "12+"])}
+    out["tail_rays_by_hit_before"] = {"no": {"rays": bh[0], "nodes_per_ray": round(bh[1] / max(1, bh[0]), 2)},
+                                      "yes": {"rays": bh[2], "nodes_per_ray": round(bh[3] / max(1, bh[2]), 2)}}
     out["skip_camera"] = os.environ.get("PT_SECTIONS_SKIP_CAMERA") is not None
     print(json.dumps(out, indent=1))
     if args.out:
