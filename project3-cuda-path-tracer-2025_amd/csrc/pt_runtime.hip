@@ -66,6 +66,7 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
     for (int i = t; i < rows * NSEG; i += blockDim.x) {
         (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
         (&ctl->qcnt[0][0][0])[i * CNT_PAD + 1] = 0;   // handed-over traversals
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD + 2] = 0;   // ... and those taken by k_bvh_tail_trav
     }
     __syncthreads();
     if (t == 0) {
@@ -634,25 +635,20 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
 }
 
 // The handed-over traversals, run by a fixed grid of waves that refill their lanes as rays
-// finish.  Wave w of segment s takes the entries [w * per, (w + 1) * per) of the
-// segment (per >= 64, from the segment's count: no atomics); whenever `refill` or more lanes are
-// idle it loads the next entries into them, so a wave drains once per range instead of once per
-// 64 rays.  Traversal only: a finished ray's result (t, u, v, triangle) replaces its saved hit,
-// and k_bvh_tail_shade shades the entries in full waves.  No barrier: waves leave on their own.
+// finish: whenever `refill` or more of a wave's lanes are idle, it takes that many entries of its
+// segment from the segment's counter of taken entries (FrameCtl::qcnt[b][s][2]; one atomic per
+// refill), so a wave drains once, when its segment is done, instead of once per 64 rays.
+// Traversal only: a finished ray's result (t, u, v, triangle) replaces its saved hit, and
+// k_bvh_tail_shade shades the entries in full waves.  No barrier: waves leave on their own.
 template <int VAR>
 __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc, QueueBuf q, TailBuf t, FrameCtl* ctl,
-                                                                    int bounce, int refill, int min_range) {
+                                                                    int bounce, int refill) {
     extern __shared__ float4 s_dyn[];
     int* s_stack = reinterpret_cast<int*>(s_dyn) + threadIdx.x;
     const int seg = blockIdx.x & (NSEG - 1);
     const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
-    const int waves = (gridDim.x / NSEG) * (BLOCK / 64);
-    const int w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x / NSEG) * (BLOCK / 64) + (int)(threadIdx.x >> 6));
-    const int used = max(1, min(waves, (n + min_range - 1) / min_range));
-    const int per = (n + used - 1) / used;
-    int next = w * per;
-    const int hi = min(n, next + per);
-    if (w >= used || next >= hi) return;   // wave-uniform
+    if (n == 0) return;
+    int next = 0;   // the segment's next untaken entry, as of this wave's last refill
     constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
     int e = -1, qs = 0, n_nodes = 0, n_tris = 0, sp0 = 0;
     bool hit0 = false;
@@ -661,10 +657,14 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
     while (true) {
         const uint64_t idle = __ballot(e < 0);
         const int n_idle = __popcll(idle);
-        if (next < hi && (n_idle >= refill || n_idle == 64)) {
+        if (next < n && (n_idle >= refill || n_idle == 64)) {
+            const int lead = __builtin_ctzll(idle);
+            int b0 = 0;
+            if ((int)(threadIdx.x & 63) == lead) b0 = atomicAdd(&ctl->qcnt[bounce][seg][2], n_idle);
+            next = __builtin_amdgcn_readlane(b0, lead);
             if (e < 0) {
                 const int k = next + mbcnt(idle);
-                if (k < hi) {
+                if (k < n) {
                     e = seg * t.stride + k;
                     const int2 nd = t.node[e];
                     qs = nd.x;
@@ -1167,7 +1167,7 @@ struct State {
     QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
     TailBuf tail{};                  // the traversals k_bvh_bounce hands to k_bvh_tail_trav
     int tail_lanes = 0;              // bvh_tail_lanes()
-    int tail_refill = 16, tail_trav_blocks = 224, tail_min_range = 64;   // PT_BVH_TAIL_REFILL / _TRAV_BLOCKS / _MIN_RANGE
+    int tail_refill = 16, tail_trav_blocks = 224;   // PT_BVH_TAIL_REFILL / _TRAV_BLOCKS
     int tail_depth = 0;              // stack entries per handed-over traversal
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
@@ -1315,7 +1315,7 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
                gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
         if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
             launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
-                   gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill, gp->tail_min_range);
+                   gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
             launch(400 + b, k_bvh_tail_shade<VAR>, dim3(NSEG * nblocks(gp->tail.stride)), dim3(BLOCK), 0, gp->sc,
                    gp->queue, gp->tail, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
         }
@@ -1979,7 +1979,7 @@ int q_stride_for(int frames) {
 // are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56)
 int bvh_tail_lanes() {
     const char* e = getenv("PT_BVH_TAIL_LANES");
-    return std::min(56, std::max(0, e ? atoi(e) : 24));
+    return std::min(56, std::max(0, e ? atoi(e) : 32));
 }
 // entries per tail segment: what k_bvh_bounce can hand over, `lanes` per wave of its blocks of one
 // segment.  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane that finds its segment
@@ -2034,7 +2034,6 @@ int ensure_frames(int frames) {
         gp->tail_lanes = bvh_tail_lanes();
         gp->tail_refill = getenv("PT_BVH_TAIL_REFILL") ? std::max(1, std::min(64, atoi(getenv("PT_BVH_TAIL_REFILL")))) : 16;
         gp->tail_trav_blocks = getenv("PT_BVH_TAIL_TRAV_BLOCKS") ? std::max(1, atoi(getenv("PT_BVH_TAIL_TRAV_BLOCKS"))) : 224;
-        gp->tail_min_range = getenv("PT_BVH_TAIL_MIN_RANGE") ? std::max(64, atoi(getenv("PT_BVH_TAIL_MIN_RANGE"))) : 64;
         if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
             gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
             TailBuf& t = gp->tail;

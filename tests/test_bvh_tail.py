@@ -2,8 +2,8 @@
 
 Once no more than PT_BVH_TAIL_LANES lanes of a traversal wave are still traversing, those rays'
 traversal state (best hit, next node, stack) is written out; k_bvh_tail_trav resumes them in waves
-that refill their lanes from a range of entries as rays finish (PT_BVH_TAIL_REFILL idle lanes at a
-time), and k_bvh_tail_shade shades them in full waves.  The result must not depend on where a
+that refill their lanes from the segment's shared counter as rays finish (PT_BVH_TAIL_REFILL idle
+lanes at a time), and k_bvh_tail_shade shades them in full waves.  The result must not depend on where a
 traversal was cut or which wave finished it: every setting below renders the mesh scenes
 bit-identical to the oracle (the reference's DFS order), live counts included, through
 multi-frame passes and single API frames.  A tail segment holds at most PT_BVH_TAIL_CHUNKS x 256
@@ -23,7 +23,7 @@ def _eq(x, y):
     return np.asarray(x).tobytes() == np.asarray(y).tobytes()
 
 
-@pytest.mark.parametrize("lanes,chunks,refill", [(0, 0, 16), (1, 0, 16), (24, 0, 16), (56, 0, 1), (24, 0, 64),
+@pytest.mark.parametrize("lanes,chunks,refill", [(0, 0, 16), (1, 0, 16), (32, 0, 16), (56, 0, 1), (24, 0, 64),
                                                  (32, 1, 16), (8, 1, 64)])
 @pytest.mark.parametrize("name,res,depth", [("cornell_obj_bnnuy", (96, 96), None),
                                             ("cornell_obj_khaslana", (64, 64), 12)])
