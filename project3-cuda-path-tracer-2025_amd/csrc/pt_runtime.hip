@@ -705,39 +705,40 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
         }
     }
 }
-// ... and their shading, gather and compaction, as k_bvh_bounce's (block (j, s) = blockIdx
-// (j * NSEG + s): entries j * BLOCK .. of segment s, survivors to output segment s)
+// ... and their shading, gather and compaction, as k_bvh_bounce's: block b takes the chunks
+// j = b / NSEG, + gridDim / NSEG, .. of BLOCK entries of segment s = b % NSEG, survivors to output
+// segment s (a grid for the usual counts, not for the capacity: empty blocks cost dispatch time)
 template <int VAR>
 __global__ __launch_bounds__(BLOCK) void k_bvh_tail_shade(SceneDev sc, QueueBuf q, TailBuf t, PathBuf out, FrameCtl* ctl,
                                                           float* __restrict__ image, int bounce, int seg_stride) {
     const int seg = blockIdx.x & (NSEG - 1);
     const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
-    const int block_start = (blockIdx.x / NSEG) * BLOCK;
-    if (block_start >= n) return;
     const int iter = ctl->iter;
     const bool to_plane = ctl->batch > 1 || ctl->plane != 0;
     const int tid = threadIdx.x;
-    const bool active = block_start + tid < n;
-    PathReg p;
-    p.rb = 0;
-    if (active) {
-        const int e = seg * t.stride + block_start + tid;
-        const int qs = t.node[e].x;
-        const float4 a = q.A[qs], b = q.B[qs], h = t.hit[e];
-        p.o = mk(a.x, a.y, a.z);
-        p.d = mk(b.x, b.y, b.z);
-        TravState st;
-        st.t_hit = h.x;
-        st.bu = h.y;
-        st.bv = h.z;
-        st.btri = __float_as_int(h.w);
-        bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
+    for (int block_start = (blockIdx.x / NSEG) * BLOCK; block_start < n; block_start += (gridDim.x / NSEG) * BLOCK) {
+        const bool active = block_start + tid < n;
+        PathReg p;
+        p.rb = 0;
+        if (active) {
+            const int e = seg * t.stride + block_start + tid;
+            const int qs = t.node[e].x;
+            const float4 a = q.A[qs], b = q.B[qs], h = t.hit[e];
+            p.o = mk(a.x, a.y, a.z);
+            p.d = mk(b.x, b.y, b.z);
+            TravState st;
+            st.t_hit = h.x;
+            st.bu = h.y;
+            st.bv = h.z;
+            st.btri = __float_as_int(h.w);
+            bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
+        }
+        const bool surv = active && p.rb > 0;
+        if (active && !surv) gather_into_image(image, sc, to_plane, p);
+        int si, unused;
+        block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
+        if (surv) store_path(out, seg * seg_stride + si, p);
     }
-    const bool surv = active && p.rb > 0;
-    if (active && !surv) gather_into_image(image, sc, to_plane, p);
-    int si, unused;
-    block_append<false>(surv, &ctl->cnt[bounce + 1][seg][0], false, nullptr, si, unused);
-    if (surv) store_path(out, seg * seg_stride + si, p);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1167,7 +1168,7 @@ struct State {
     QueueBuf queue{};                // its traversal queue (capacity: one pass's paths)
     TailBuf tail{};                  // the traversals k_bvh_bounce hands to k_bvh_tail_trav
     int tail_lanes = 0;              // bvh_tail_lanes()
-    int tail_refill = 16, tail_trav_blocks = 224;   // PT_BVH_TAIL_REFILL / _TRAV_BLOCKS
+    int tail_refill = 16, tail_trav_blocks = 224, tail_shade_blocks = 512;   // PT_BVH_TAIL_REFILL / _TRAV_BLOCKS / _SHADE_BLOCKS
     int tail_depth = 0;              // stack entries per handed-over traversal
     // one captured pass per pass size (1..MAXF frames)
     hipGraph_t graph[MAXF + 1] = {};
@@ -1316,7 +1317,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
         if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
             launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
                    gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
-            launch(400 + b, k_bvh_tail_shade<VAR>, dim3(NSEG * nblocks(gp->tail.stride)), dim3(BLOCK), 0, gp->sc,
+            const int per_seg = gp->tail_shade_blocks > 0 ? std::min(gp->tail_shade_blocks, nblocks(gp->tail.stride))
+                                                          : nblocks(gp->tail.stride);
+            launch(400 + b, k_bvh_tail_shade<VAR>, dim3(NSEG * per_seg), dim3(BLOCK), 0, gp->sc,
                    gp->queue, gp->tail, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
         }
     }
@@ -2034,6 +2037,7 @@ int ensure_frames(int frames) {
         gp->tail_lanes = bvh_tail_lanes();
         gp->tail_refill = getenv("PT_BVH_TAIL_REFILL") ? std::max(1, std::min(64, atoi(getenv("PT_BVH_TAIL_REFILL")))) : 16;
         gp->tail_trav_blocks = getenv("PT_BVH_TAIL_TRAV_BLOCKS") ? std::max(1, atoi(getenv("PT_BVH_TAIL_TRAV_BLOCKS"))) : 224;
+        gp->tail_shade_blocks = getenv("PT_BVH_TAIL_SHADE_BLOCKS") ? atoi(getenv("PT_BVH_TAIL_SHADE_BLOCKS")) : 512;
         if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
             gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
             TailBuf& t = gp->tail;
