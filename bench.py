@@ -49,15 +49,28 @@ STATE_BYTES = 48               # one path in flight: 3 x float4 (origin|pixel, d
 IMAGE_RMW_BYTES = 24           # terminated path: read + write its pixel's float3 (1-frame pass)
 PLANE_STORE_BYTES = 12         # terminated path of an F-frame pass: float3 store to its frame's plane
 QUEUE_ENTRY_BYTES = 64         # mesh scenes: a ray queued for k_bvh_bounce (written by k_bounce, read back)
+# mesh scenes: a traversal handed over by k_bvh_bounce: its state (queue slot + saved node 8 B, best hit 16 B,
+# 4 B per stack entry) written and read back by k_bvh_tail_trav, its final hit (16 B) written there, slot and
+# hit read again by k_bvh_tail_shade (24 B), and the queue entry re-read (the ray, 32 B, by the traversal; all
+# 64 B by the shading): 24 + 24 + 16 + 24 + 32 + 64 = 184 B + 8 B per stack entry
+HANDOVER_BYTES = 184
+HANDOVER_STACK_BYTES = 8
 N_CUS = 256                    # MI355X compute units
 
-# BASELINE.json configs[2..4] as sub-records of the N=1 line: (tag, scene, res, depth, sort, pipeline, steps, warmup)
+# BASELINE.json configs[2..4] as sub-records of the N=1 line: (tag, scene, res, depth, sort, pipeline, steps, warmup
+# [, options]), then the reference's large-mesh scenes (cornell_obj_cyrene.json:266, README.md:206; 262k / 1.0M
+# triangle stand-ins) on the pair layout and, for comparison, on the node-array traversal they took until round 5
+VAR_NODE_ARRAY = 186 | 64      # the default variant + VAR_BVH_NODES (no pair layout, no traversal queue)
 SUB_CONFIGS = [
     ("configs[2]", "cornell_glass_test.json", None, None, True, "fused", 48, 4),
     ("configs[2] staged", "cornell_glass_test.json", None, None, True, "staged", 48, 4),
     ("configs[2] sort off", "cornell_glass_test.json", None, None, False, "fused", 48, 4),
     ("configs[3]", "cornell_obj_bnnuy.json", None, None, False, "fused", 48, 4),
     ("configs[4]", "cornell_obj_khaslana.json", (1600, 1600), 12, False, "fused", 32, 2),
+    ("mesh 262k", "cornell_obj_cyrene.json", None, None, False, "fused", 24, 2),
+    ("mesh 262k node array", "cornell_obj_cyrene.json", None, None, False, "fused", 8, 1, {"variant": VAR_NODE_ARRAY}),
+    ("mesh 1.0M", "cornell_obj_phainon.json", None, None, False, "fused", 24, 2),
+    ("mesh 1.0M node array", "cornell_obj_phainon.json", None, None, False, "fused", 8, 1, {"variant": VAR_NODE_ARRAY}),
 ]
 
 
@@ -71,6 +84,7 @@ def parse():
     ap.add_argument("--sort", action="store_true", help="material sort (MATERIAL_SORTING, configs[2])")
     ap.add_argument("--res", default="", help="WxH override (configs[4]: 1600x1600)")
     ap.add_argument("--depth", type=int, default=-1, help="trace depth override (configs[4]: 12)")
+    ap.add_argument("--variant", type=int, default=-1, help="kernel variant bits (A/B; default: the library's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[2..4] sub-records")
     ap.add_argument("--no-api", action="store_true", help="skip the single-frame pt_trace() timing")
@@ -219,6 +233,8 @@ def main():
     pixels = world > 1 and args.shard == "pixels"
     rows = shard_rows(scene.height, world) if pixels else 8
     shard = dict(shard_mode=ptamd.SHARD_PIXELS, shard_rank=rank, shard_count=world, shard_rows=rows) if pixels else {}
+    if args.variant >= 0:
+        shard["variant"] = args.variant
     tr = ptamd.PathTracer(scene, device=device, pipeline=pipeline, material_sort=int(args.sort), **shard)
     depth = scene.trace_depth
 
@@ -364,11 +380,12 @@ def kernels_digest(prof, spread):
 def sub_config(ptamd, cfg):
     """One BASELINE config on this GPU: warmup, K timed frames (pass graphs), eager profiled
     replay for its roofline.  Same timing rules as the headline."""
-    tag, scene_name, res, depth, sort, pipeline, steps, warmup = cfg
+    tag, scene_name, res, depth, sort, pipeline, steps, warmup = cfg[:8]
+    opts = cfg[8] if len(cfg) > 8 else {}
     path = os.path.join(REPO, "scenes", scene_name)
     sc = ptamd.SceneFile(path, res=res, depth=depth)
     tr = ptamd.PathTracer(sc, pipeline=ptamd.PIPELINE_STAGED if pipeline == "staged" else ptamd.PIPELINE_FUSED,
-                          material_sort=int(sort))
+                          material_sort=int(sort), **opts)
     it = 1
     tr.trace_frames(it, warmup)
     it += warmup
@@ -399,6 +416,14 @@ def sub_config(ptamd, cfg):
                                               "staged_c2" if pipeline == "staged" and "glass" in scene_name and sort
                                               else None)),
            "kernels": kernels_digest(prof, None)}
+    if "obj" in scene_name:
+        out["triangles"] = len(sc.triangles)
+        q = sum(st["queued_total"])
+        out["queued_share"] = round(q / max(1, st["segments_total"]), 4)      # paths that enter the mesh
+        out["handed_share"] = round(sum(st["handed_total"]) / max(1, q), 4)   # ... of those, handed over
+        out["handed_stack_mean"] = round(sum(st["handed_stack_total"]) / max(1, sum(st["handed_total"])), 2)
+    if opts:
+        out["options"] = opts
     if tag == "configs[4]":
         out["note"] = "BASELINE names 8 GPUs for this config; this sub-record is one GPU (bench.py --gpus 8 --scene ...)"
     tr.free()
@@ -444,13 +469,13 @@ def api_frame_ms(tr, first_iteration, frames=40, warm=5):
         return round(ts[len(ts) // 2], 4), round(ts[int(0.9 * (len(ts) - 1))], 4)
     m_copy, p_copy = run(True, first_iteration)
     m_nc, p_nc = run(False, first_iteration + warm + frames)
-    # the same calls with the next-frame speculation off (PT_SPECULATE=0, read per call): every
-    # frame traced inside its own call, strictly before its copy
-    os.environ["PT_SPECULATE"] = "0"
+    # the same calls with the next-frame speculation off (pt_set_speculation(0)): every frame
+    # traced inside its own call, strictly before its copy
+    tr.set_speculation(False)
     try:
         m_ns, p_ns = run(True, first_iteration + 2 * (warm + frames))
     finally:
-        del os.environ["PT_SPECULATE"]
+        tr.set_speculation(True)
     return {"ms_per_frame": m_copy, "p90": p_copy, "ms_per_frame_no_copy": m_nc, "p90_no_copy": p_nc,
             "ms_per_frame_no_speculation": m_ns, "p90_no_speculation": p_ns,
             "frames": frames, "note": "pt_trace(F=1) + 7.68 MB D->H into the caller's pageable host memory per call; "
@@ -474,6 +499,8 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
     (hipExtLaunchKernel dispatch timestamps, pt_profile_frames)."""
     tot = st["live_total"]                 # per-bounce live counts summed over the timed frames
     queued = st.get("queued_total") or [0] * len(tot)
+    handed = st.get("handed_total") or [0] * len(tot)
+    handed_stack = st.get("handed_stack_total") or [0] * len(tot)
     launches = depth * prof["passes"]
     nbytes = 0
     for b in range(depth):
@@ -482,6 +509,7 @@ def roofline(prof, st, pipeline, steps, depth, headline=True, traffic_file=None)
             gather = IMAGE_RMW_BYTES if st["frames_per_pass"] == 1 else PLANE_STORE_BYTES
             nbytes += (STATE_BYTES * n_in if b > 0 else 0) + STATE_BYTES * n_out + gather * (n_in - n_out)
             nbytes += 2 * QUEUE_ENTRY_BYTES * queued[b]      # traversal queue round trip
+            nbytes += HANDOVER_BYTES * handed[b] + HANDOVER_STACK_BYTES * handed_stack[b]   # hand-over
         else:
             nbytes += 4 * n_in + 2 * STATE_BYTES * n_out
     if pipeline == "fused" and any(prof["bvh_ms"][:depth]):

@@ -34,8 +34,9 @@ extern "C" {
 #endif
 
 /* 2: pt_options gained num_devices / device_ids / combine, pt_frame_stats queued_total,
- *    pt_kernel_times tail_ms / tail_from; pt_set_trace_depth */
-#define PT_ABI_VERSION 2
+ *    pt_kernel_times tail_ms / tail_from; pt_set_trace_depth
+ * 3: pt_frame_stats handed_total / handed_stack_total; pt_set_speculation */
+#define PT_ABI_VERSION 3
 #define PT_MAX_DEVICES 16
 
 enum {
@@ -131,6 +132,8 @@ typedef struct pt_frame_stats {
     int32_t last_pass_frames;
     int64_t queued_total[65];    /* mesh scenes, fused pipeline: per-bounce paths queued for the BVH
                                     traversal kernel, summed over frames_total frames (0 otherwise) */
+    int64_t handed_total[65];    /* ... of those, traversals handed over to the refilling waves */
+    int64_t handed_stack_total[65];  /* ... and the stack entries they carried */
 } pt_frame_stats;
 
 int32_t pt_abi_version(void);
@@ -166,7 +169,10 @@ int32_t pt_prepare_frames(int32_t count);
 /* Block until all queued work finished. */
 int32_t pt_synchronize(void);
 
-/* Accumulated image: host copy (n_floats >= width*height*3) / raw device pointer. */
+/* Accumulated image: host copy (n_floats >= width*height*3) / raw device pointer.  The caller may
+ * read or write through the device pointer between pt_trace calls: pt_get_image_device drops a
+ * speculated next frame (pt_trace with a host copy traces frame N + 1 ahead from the image as it
+ * was), so the next pt_trace traces from whatever the caller left in the buffer. */
 int32_t pt_get_image(float* host_out, int64_t n_floats);
 int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats);
 /* Overwrite the accumulated image (host data), e.g. after a multi-GPU reduce. */
@@ -188,6 +194,10 @@ int32_t pt_set_camera(const pt_camera* camera);
 /* RenderState::traceDepth, re-read by the reference at every pathtrace() call (pathtrace.cu:641):
  * the depth of the next frames (0 .. 64); resets nothing else. */
 int32_t pt_set_trace_depth(int32_t depth);
+/* Next-frame speculation of single-frame calls that copy the image out (pt_trace with host_image:
+ * frame N + 1 is traced while frame N's image crosses PCIe; results bit-identical either way).
+ * On by default (PT_SPECULATE=0 in the environment at pt_init: off); off drops a speculated frame. */
+int32_t pt_set_speculation(int32_t enabled);
 
 /* ---- scene ingest (C++ restatement of scene.cpp, host/scene.cpp) for non-C++ callers ---- */
 typedef struct pt_scene_file pt_scene_file;

@@ -74,6 +74,7 @@ struct SceneDev {
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
+    int ref_shift;            // pair-layout stack entries: ref << ref_shift | T field (pack_ref)
     float4 root_lo, root_hi;  // root box (w: root s)
     float cull_c0;            // c = s^2 * cull_c0 (64 2^-24 / 1e-5, rounded up)
     float cull_E;             // scene extent (rounded up): cE = c * cull_E
@@ -105,6 +106,8 @@ struct FrameCtl {
     unsigned long long frames;              // frames started since the last stats reset
     unsigned long long tot[MAXB + 1];       // sum over finished frames of paths entering bounce b
     unsigned long long qtot[MAXB + 1];      // the same for qcnt (paths of bounce b queued for traversal)
+    unsigned long long htot[MAXB + 1];      // ... traversals handed over to k_bvh_tail_trav (qcnt[b][s][3])
+    unsigned long long hstk[MAXB + 1];      // ... their saved stack entries (qcnt[b][s][4])
     int cnt[MAXB + 1][NSEG][CNT_PAD];       // paths entering bounce b, per output segment ([..][0])
     // VAR_BVH_SPLIT: paths of bounce b queued for traversal, per queue segment (blockIdx % NSEG of
     // the queuing k_bounce block).  One counter per segment, not one for the whole queue: every
@@ -414,7 +417,7 @@ PT_DEV float bvh_intersect_fast(const SceneDev& sc, f3 ro, f3 rd, int* stack, fl
 //  * the node being expanded is a 64-B DevPair of its children: one record fetch yields both
 //    boxes (exact-decision aabb_decide), their refs and their cull sizes;
 //  * the nearer accepted child is expanded next without touching the stack; the farther one is
-//    pushed as [ref:16 | T:bf16], where T is the cull threshold of node_culled solved for t_best
+//    pushed as [ref | T] (pack_ref), where T is the cull threshold of node_culled solved for t_best
 //    (culled iff t_best < T, T rounded down), so a pop needs no fetch to decide the cull;
 //  * leaf triangles live in 4-slot groups in reference visit order: ties on t go to the smaller
 //    hot4 index, i.e. to the triangle the reference meets first.
@@ -427,7 +430,22 @@ PT_DEV float cull_threshold(const SceneDev& sc, float entry, float s) {
     const float T = num * __builtin_amdgcn_rcpf(1.0f + 2.0f * c + 2e-6f) * (1.0f - 1e-6f);
     return T > 0.0f ? T : 0.0f;      // NaN (inf - inf on degenerate data) -> 0: never culled
 }
-PT_DEV uint32_t pack_ref(int ref, float T) { return ((uint32_t)ref << 16) | (__float_as_uint(T) >> 16); }
+// Stack entry of the pair layout: [ref : 32 - S | T field : S], S = SceneDev::ref_shift (the
+// fewest ref bits the tree's P + L refs need, so small trees keep more of T).  The field holds the
+// top S bits of u = clamp(bits(T), T_BIAS, T_BIAS + 2^30 - 1) - T_BIAS, i.e. T's exponent from
+// 2^-17 to 2^111 and as much mantissa as fits; truncation rounds T down, which only culls less.
+// Below 2^-17 the field is 0 and decodes to 2^-17: a cull then needs t_best < 2^-17, and with
+// t_best below 1e-5 no triangle can be accepted at all (tri_test_e rejects t <= 1e-5), so such a
+// cull never changes a result.  Refs up to 2^24 - 1 (S >= 8).
+constexpr uint32_t T_BIAS = 0x37000000u;   // bits of 2^-17
+PT_DEV uint32_t pack_ref(int ref, float T, int S) {
+    const uint32_t b = __float_as_uint(T);
+    const uint32_t u = __builtin_elementwise_min(__builtin_elementwise_max(b, T_BIAS), T_BIAS + 0x3fffffffu) - T_BIAS;
+    return ((uint32_t)ref << S) | (u >> (30 - S));
+}
+PT_DEV float unpack_T(uint32_t w, int S) {
+    return __uint_as_float((__builtin_amdgcn_ubfe(w, 0, S) << (30 - S)) + T_BIAS);
+}
 // cull_threshold from the per-child constants the host packs into DevPair's hi.w (pack_cull in
 // pt_runtime.hip): high half A >= 1.002 c s + c E (1 + 1e-6), low half d >= 1 - (1 - 1e-6) /
 // (1 + 2c + 2e-6), both rounded UP to 16-bit floats.  T = (entry (1 - 2e-6) - A)(1 - d), two fmas
@@ -478,14 +496,15 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
                  : -1;
 }
 // pop the nearest stack entry whose certified cull does not reject it (st.cur = -1: empty)
-PT_DEV void trav_pop(TravState& st, int* stack) {
+PT_DEV void trav_pop(const SceneDev& sc, TravState& st, int* stack) {
     const float tb = st.t_hit;
+    const int S = sc.ref_shift;
     st.cur = -1;
     while (st.sp > 0) {
         const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
-        const float T = __uint_as_float(w << 16);
+        const float T = unpack_T(w, S);
         if (!(tb < T)) {
-            st.cur = (int)(w >> 16);
+            st.cur = (int)(w >> S);
             st.curT = T;
             break;
         }
@@ -525,7 +544,7 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
         st.curT = lfirst ? Tl : Tr;
         const int far = lfirst ? rrf : rl;
         const float Tf = lfirst ? Tr : Tl;
-        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf);
+        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf, sc.ref_shift);
         return true;
     }
     if (pl | pb) {
@@ -576,7 +595,7 @@ PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_node
     } else {
         trav_leaf<COUNT>(sc, st, st.cur - P, n_nodes, n_tris);
     }
-    if (!next) trav_pop(st, stack);
+    if (!next) trav_pop(sc, st, stack);
 }
 // result of a finished traversal: t (-1: no triangle), u, v, hot4 slot (-1)
 PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
@@ -597,15 +616,16 @@ PT_DEV float trav_result(const TravState& st, float& bu, float& bv, int& btri) {
 PT_DEV float4 trav_saved_hit(const TravState& st) {
     return make_float4(st.t_hit, st.bu, st.bv, __int_as_float(st.btri));
 }
-PT_DEV int trav_saved_node(const TravState& st) { return (st.cur & 0xffff) | (st.sp << 16); }   // refs < 2^16
+// node to expand next (refs < 2^24) | stack depth (<= MAXSTACK) << 24
+PT_DEV int trav_saved_node(const TravState& st) { return st.cur | (st.sp << 24); }
 PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node) {
     trav_ray(st, ro, rd);
     st.t_hit = hit.x;
     st.bu = hit.y;
     st.bv = hit.z;
     st.btri = __float_as_int(hit.w);
-    st.cur = node & 0xffff;
-    st.sp = node >> 16;
+    st.cur = node & 0xffffff;
+    st.sp = node >> 24;
     st.curT = 0.f;
 }
 // expand nodes until the ray is finished (st.cur < 0) or -- defer > 0 -- until no more than

@@ -56,9 +56,15 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
             unsigned long long s = 0;
             for (int k = 0; k < NSEG; ++k) s += (unsigned)ctl->cnt[b][k][0];
             ctl->tot[b] += s;
-            unsigned long long q = 0;
-            for (int k = 0; k < NSEG; ++k) q += (unsigned)ctl->qcnt[b][k][0];
+            unsigned long long q = 0, h = 0, hs = 0;
+            for (int k = 0; k < NSEG; ++k) {
+                q += (unsigned)ctl->qcnt[b][k][0];
+                h += (unsigned)ctl->qcnt[b][k][3];
+                hs += (unsigned)ctl->qcnt[b][k][4];
+            }
             ctl->qtot[b] += q;
+            ctl->htot[b] += h;
+            ctl->hstk[b] += hs;
         }
     }
     __syncthreads();
@@ -67,6 +73,8 @@ __global__ void k_frame_begin(FrameCtl* ctl, int set_iter, int local_pixels, int
         (&ctl->qcnt[0][0][0])[i * CNT_PAD] = 0;
         (&ctl->qcnt[0][0][0])[i * CNT_PAD + 1] = 0;   // handed-over traversals
         (&ctl->qcnt[0][0][0])[i * CNT_PAD + 2] = 0;   // ... and those taken by k_bvh_tail_trav
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD + 3] = 0;   // handed-over traversals stored (stats)
+        (&ctl->qcnt[0][0][0])[i * CNT_PAD + 4] = 0;   // ... and their stack entries (stats)
     }
     __syncthreads();
     if (t == 0) {
@@ -155,13 +163,18 @@ __global__ __launch_bounds__(BLOCK) void k_adopt_frame(const float* __restrict__
         for (int i = t; i < rows * NSEG; i += BLOCK) {
             int* c = &ctl->cnt[0][0][0] + i * CNT_PAD;
             int* q = &ctl->qcnt[0][0][0] + i * CNT_PAD;
-            const int c0 = *c, q0 = *q;
-            const int c1 = (&spec->cnt[0][0][0])[i * CNT_PAD], q1 = (&spec->qcnt[0][0][0])[i * CNT_PAD];
+            const int c0 = *c, q0 = q[0], h0 = q[3], hs0 = q[4];
+            const int* qs = &spec->qcnt[0][0][0] + i * CNT_PAD;
+            const int c1 = (&spec->cnt[0][0][0])[i * CNT_PAD], q1 = qs[0], h1 = qs[3], hs1 = qs[4];
             const int b = i / NSEG;
             if (fold && c0) atomicAdd(&ctl->tot[b], (unsigned long long)(unsigned)c0);
             if (fold && q0) atomicAdd(&ctl->qtot[b], (unsigned long long)(unsigned)q0);
+            if (fold && h0) atomicAdd(&ctl->htot[b], (unsigned long long)(unsigned)h0);
+            if (fold && hs0) atomicAdd(&ctl->hstk[b], (unsigned long long)(unsigned)hs0);
             *c = c1;
-            *q = q1;
+            q[0] = q1;
+            q[3] = h1;
+            q[4] = hs1;
         }
         __syncthreads();   // every thread read `frames` before it changes
         if (t == 0) {
@@ -571,6 +584,10 @@ PT_DEV bool tail_put(const TailBuf& t, int* ctr, int seg, int qs, const TravStat
     t.node[e] = make_int2(qs, trav_saved_node(st));
     t.hit[e] = trav_saved_hit(st);
     for (int i = 0; i < st.sp; ++i) t.stack[(size_t)i * t.cap + e] = s_stack[i * BLOCK];
+    // stats (pt_frame_stats handed_total / handed_stack_total): same-address atomics, one per
+    // wave after the compiler's wave reduction, on the counter line the reservation just used
+    atomicAdd(ctr + 2, 1);
+    atomicAdd(ctr + 3, st.sp);
     return true;
 }
 
@@ -1118,8 +1135,61 @@ constexpr int MAXF = 256;                   // frames per pass, upper bound (slo
 // buffers + 5.2 GB traversal queue at 1600^2, F = 32 (of 288 GB).
 constexpr int64_t AUTO_BATCH_PATHS = 84000000;
 
+// Tuning and test knobs (tools, A/B runs, tests).  Every one is read from the environment in ONE
+// place, read_tuning(), when pt_init builds a context -- never on a hot call -- and none changes a
+// result (the tests run each one against the oracle).  INTEGRATION.md §5 lists them.
+struct Tuning {
+    size_t bounce_lds_pad = 0, bvh_lds_pad = 0;   // PT_BOUNCE_LDS_PAD / PT_BVH_LDS_PAD: unused LDS (occupancy A/B)
+    bool sections_skip_camera = false;              // PT_SECTIONS_SKIP_CAMERA: camera bounce out of the counters
+    bool tail_off = false;                          // PT_TAIL=0: no k_tail launch
+    bool tail_any_batch = false;                    // PT_TAIL_BATCH=1: k_tail for multi-frame passes too
+    int tail_from = 0;                              // PT_TAIL_FROM: k_tail's first bounce (0: depth / 2)
+    int64_t auto_paths = 0;                         // PT_AUTO_PATHS: auto pass size in paths (0: AUTO_BATCH_PATHS)
+    bool f1_graph = false;                          // PT_F1_GRAPH=1: single-frame passes through a graph
+    bool multi_f1_direct = false;                   // PT_MULTI_F1_DIRECT=1: shards' single frames launched directly
+    int bvh_tail_lanes = 32;                        // PT_BVH_TAIL_LANES (0..56; 0: no hand-over)
+    int bvh_tail_chunks = 0;                        // PT_BVH_TAIL_CHUNKS: capped hand-over buffers (tests)
+    int tail_refill = 16;                           // PT_BVH_TAIL_REFILL (1..64 idle lanes)
+    int tail_trav_blocks = 224;                     // PT_BVH_TAIL_TRAV_BLOCKS per segment
+    int tail_shade_blocks = 512;                    // PT_BVH_TAIL_SHADE_BLOCKS per segment (0: one per chunk)
+    bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
+    bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
+    bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
+    int grid = -1;                                  // PT_GRID: 0 no candidate table, 1 also for small scenes
+    bool speculate = true;                          // PT_SPECULATE=0: initial state of pt_set_speculation
+};
+Tuning read_tuning() {
+    auto num = [](const char* name, long dflt) {
+        const char* e = getenv(name);
+        return e && *e ? atol(e) : dflt;
+    };
+    Tuning t;
+    t.bounce_lds_pad = (size_t)std::max(0L, num("PT_BOUNCE_LDS_PAD", 0));
+    t.bvh_lds_pad = (size_t)std::max(0L, num("PT_BVH_LDS_PAD", 0));
+    t.sections_skip_camera = getenv("PT_SECTIONS_SKIP_CAMERA") != nullptr;
+    t.tail_off = num("PT_TAIL", 1) == 0;
+    t.tail_any_batch = num("PT_TAIL_BATCH", 0) != 0;
+    t.tail_from = (int)num("PT_TAIL_FROM", 0);
+    t.auto_paths = num("PT_AUTO_PATHS", 0);
+    t.f1_graph = num("PT_F1_GRAPH", 0) != 0;
+    t.multi_f1_direct = num("PT_MULTI_F1_DIRECT", 0) != 0;
+    t.bvh_tail_lanes = (int)std::min(56L, std::max(0L, num("PT_BVH_TAIL_LANES", 32)));
+    t.bvh_tail_chunks = (int)std::max(0L, num("PT_BVH_TAIL_CHUNKS", 0));
+    t.tail_refill = (int)std::max(1L, std::min(64L, num("PT_BVH_TAIL_REFILL", 16)));
+    t.tail_trav_blocks = (int)std::max(1L, num("PT_BVH_TAIL_TRAV_BLOCKS", 224));
+    t.tail_shade_blocks = (int)std::max(0L, num("PT_BVH_TAIL_SHADE_BLOCKS", 512));
+    t.combine_force_staged = num("PT_COMBINE_FORCE_STAGED", 0) != 0;
+    const char* tree = getenv("PT_BVH_TREE");
+    t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
+    t.bvh_tree_info = getenv("PT_BVH_TREE_INFO") != nullptr;
+    t.grid = (int)num("PT_GRID", -1);
+    t.speculate = num("PT_SPECULATE", 1) != 0;
+    return t;
+}
+
 struct State {
     bool inited = false;
+    Tuning tune;
     pt_options opts{};
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1302,12 +1372,11 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
     const size_t stack_lds = HAS_BVH && !SPLIT ? gp->bvh_lds : 0;
     // VAR_MAT_GROUP's exchange reuses the exact-test exchange's region (it runs after it)
     const size_t xchg_lds = (VAR & VAR_MAT_GROUP) ? std::max(redist_lds, mat_group_lds(HAS_BVH, false)) : redist_lds;
-    // tools: PT_BOUNCE_LDS_PAD / PT_BVH_LDS_PAD=<bytes> add unused LDS to k_bounce / the traversal
-    // kernel (occupancy A/B)
-    static const size_t bounce_pad = getenv("PT_BOUNCE_LDS_PAD") ? (size_t)atol(getenv("PT_BOUNCE_LDS_PAD")) : 0;
+    // tools: unused LDS added to k_bounce / the traversal kernel (occupancy A/B)
+    const size_t bounce_pad = gp->tune.bounce_lds_pad;
     launch(100 + b, k_bounce<FIRST, HAS_BVH, VAR>, grid, dim3(BLOCK), geom_lds + stack_lds + xchg_lds + bounce_pad, gp->sc,
            in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
-    static const size_t lds_pad = getenv("PT_BVH_LDS_PAD") ? (size_t)atol(getenv("PT_BVH_LDS_PAD")) : 0;
+    const size_t lds_pad = gp->tune.bvh_lds_pad;
     if (SPLIT) {
         const size_t stack_bytes = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int);
         // the handed-over stacks were sized for the pair tree of the allocation (ensure_frames)
@@ -1379,8 +1448,7 @@ int effective_variant(bool first, int var) {
     // (A/B: bounce 0 0.164 -> 0.174 ms, bounces 1-7 ~6 % faster)
     if (first) var &= ~(VAR_WAVE_REDIST | VAR_BLOCK_REDIST);
     // tools: PT_SECTIONS_SKIP_CAMERA=1 leaves the camera bounce out of the section counters
-    static const bool skip_cam = getenv("PT_SECTIONS_SKIP_CAMERA") != nullptr;
-    if (first && skip_cam) var &= ~VAR_SECTION_TIMING;
+    if (first && gp->tune.sections_skip_camera) var &= ~VAR_SECTION_TIMING;
     if (!gp->split) var &= ~VAR_BVH_SPLIT;
     // the texture-free build exists for the default variants (and their section-counter and
     // material-grouping forms); other variants keep the texture code
@@ -1426,15 +1494,13 @@ void launch_compact(PathBuf pi, PathBuf po, const int* n_in, int* n_out, int npa
 // single-frame passes of primitive-only scenes run bounces tail_from() .. depth-1 as one k_tail
 // launch (PT_TAIL=0 turns it off for A/B); 0: no tail launch
 int tail_from(int batch) {
-    static const bool off = getenv("PT_TAIL") && atoi(getenv("PT_TAIL")) == 0;
     const int depth = gp->sc.trace_depth;
     const bool lds = gp->sc.num_geoms <= LDS_GEOMS;
-    static const bool any_batch = getenv("PT_TAIL_BATCH") && atoi(getenv("PT_TAIL_BATCH")) != 0;   // tools: A/B
-    if (off || (batch != 1 && !any_batch) || gp->has_bvh || !lds || depth < 3 ||
+    if (gp->tune.tail_off || (batch != 1 && !gp->tune.tail_any_batch) || gp->has_bvh || !lds || depth < 3 ||
         (effective_variant(false, gp->opts.variant) & ~VAR_NO_TEX) !=
             (VAR_CAND_QUEUE | VAR_WAVE_REDIST | VAR_BVH_FAST | VAR_BLOCK_REDIST))
         return 0;
-    static const int from = getenv("PT_TAIL_FROM") ? atoi(getenv("PT_TAIL_FROM")) : 0;   // tools: A/B
+    const int from = gp->tune.tail_from;
     return std::min(depth - 1, std::max(1, from > 0 ? from : depth / 2));
 }
 
@@ -1538,9 +1604,7 @@ int run_pass(int iter, int batch) {
     // Shards of a multi-device context replay their single-frame pass as a graph too: there the
     // host walks the shards one after another, and one graph launch per shard costs the host less
     // than six kernel launches (tools/multi_probe.py enqueue_us_per_shard)
-    static const bool f1_graph = getenv("PT_F1_GRAPH") && atoi(getenv("PT_F1_GRAPH")) != 0;
-    static const bool multi_direct = getenv("PT_MULTI_F1_DIRECT") && atoi(getenv("PT_MULTI_F1_DIRECT")) != 0;  // A/B
-    if (gp->opts.use_graph && (batch > 1 || f1_graph || (gp->multi && !multi_direct))) {
+    if (gp->opts.use_graph && (batch > 1 || gp->tune.f1_graph || (gp->multi && !gp->tune.multi_f1_direct))) {
         if (!gp->graph_exec[batch]) RC(build_graph(batch));
         // the graph's k_frame_begin advances the device iteration by one: preset iter - 1 (stream-
         // ordered) unless the last pass left it there -- main.cpp's pathtrace(pbo, 0, ++iteration)
@@ -1562,9 +1626,10 @@ int run_frame(int iter) { return run_pass(iter, 1); }
 // pageable host memory each time (pathtrace.cu:783): on MI355X that copy (~0.15 ms over PCIe) is
 // longer than the frame's kernels (~0.12 ms).  So once frame N is traced, frame N + 1 is traced
 // at once on a second stream -- into a plane of its own with a FrameCtl of its own, the accumulated
-// image untouched -- while frame N's image is copied out.  The call for iteration N + 1 then only
-// adds that plane to the image (k_add_plane: the same additions as the frame's own gathers) and
-// takes over its counters (k_adopt_frame), bit for bit what tracing it then would have produced.
+// image untouched -- while frame N's image is copied out.  At its end the frame forms image +
+// plane into a sum buffer (k_spec_sum: the same additions as the frame's own gathers); the call for
+// iteration N + 1 then copies that sum out while k_adopt_frame makes it the image and takes over
+// the frame's counters, bit for bit what tracing it then would have produced.
 // Any call that could make it differ (another iteration, a camera or depth change, multi-frame
 // passes, the test and profiling entry points) first waits for it and drops it (spec_cancel).
 // Only calls that copy the image out start one.  PT_SPECULATE=0 turns it off.  One device
@@ -1666,21 +1731,31 @@ int spec_worker_idle() {
 }
 
 bool spec_enabled() {
-    const char* e = getenv("PT_SPECULATE");   // read per call: tests and bench.py compare both
-    return !(e && atoi(e) == 0) && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED &&
+    return gp->tune.speculate && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED &&
            gp->sc.shard.mode != PT_SHARD_PIXELS;
 }
 int spec_cancel() {
     if (gp->spec_iter == 0) return PT_OK;
+    // the stream is drained even when the launcher reports an error: the launch may have failed
+    // after the graph was queued (k_spec_sum, the event), and the graph uses the pass buffers the
+    // caller's next work on gp->stream overwrites.  spec_iter is cleared once it is drained.
+    const hipError_t le = g_spec_launcher.idle();
+    const hipError_t se = hipStreamSynchronize(gp->spec_stream);
     gp->spec_iter = 0;
-    RC(spec_worker_idle());
-    HIPCHK(hipStreamSynchronize(gp->spec_stream));
+    HIPCHK(le);
+    HIPCHK(se);
     return PT_OK;
 }
 void spec_release() {
     (void)g_spec_launcher.idle();
     if (gp == &g_primary) g_spec_launcher.join();
     if (gp->spec_stream) (void)hipStreamSynchronize(gp->spec_stream);
+    // the speculated frame's graph goes with its stream (release_graph would otherwise sync a
+    // stream that no longer exists before destroying it)
+    if (gp->spec_exec) (void)hipGraphExecDestroy(gp->spec_exec);
+    if (gp->spec_graph) (void)hipGraphDestroy(gp->spec_graph);
+    gp->spec_exec = nullptr;
+    gp->spec_graph = nullptr;
     if (gp->spec_ev_in) (void)hipEventDestroy(gp->spec_ev_in);
     if (gp->spec_ev_done) (void)hipEventDestroy(gp->spec_ev_done);
     if (gp->spec_stream) (void)hipStreamDestroy(gp->spec_stream);
@@ -1747,9 +1822,14 @@ int spec_launch(int iter) {
 // stream waits for it too: the copy reads the finished sum at once, beside k_adopt_frame
 int spec_adopt(bool copy_out) {
     const int iter = gp->spec_iter;
-    RC(spec_worker_idle());   // spec_ev_done recorded
-    HIPCHK(hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0));
-    if (copy_out) HIPCHK(hipStreamWaitEvent(gp->copy_stream, gp->spec_ev_done, 0));
+    hipError_t e = g_spec_launcher.idle();   // spec_ev_done recorded
+    if (e == hipSuccess) e = hipStreamWaitEvent(gp->stream, gp->spec_ev_done, 0);
+    if (e == hipSuccess && copy_out) e = hipStreamWaitEvent(gp->copy_stream, gp->spec_ev_done, 0);
+    if (e != hipSuccess) {   // dropped: a retried call for this iteration traces it afresh
+        (void)hipStreamSynchronize(gp->spec_stream);
+        gp->spec_iter = 0;
+        HIPCHK(e);
+    }
     const int nf = 3 * gp->pixels_total;
     launch(7, k_adopt_frame, dim3(nblocks((nf + 3) / 4)), dim3(BLOCK), 0, (const float*)gp->d_spec_sum[gp->spec_sum_idx],
            gp->d_image, nf, gp->d_ctl, (const FrameCtl*)gp->d_ctl_spec, gp->ctl_rows);
@@ -1980,19 +2060,16 @@ int q_stride_for(int frames) {
 }
 // k_bvh_bounce hands a wave's traversals to k_bvh_tail_trav once no more than this many of its lanes
 // are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56)
-int bvh_tail_lanes() {
-    const char* e = getenv("PT_BVH_TAIL_LANES");
-    return std::min(56, std::max(0, e ? atoi(e) : 32));
-}
+int bvh_tail_lanes() { return gp->tune.bvh_tail_lanes; }
 // entries per tail segment: what k_bvh_bounce can hand over, `lanes` per wave of its blocks of one
 // segment.  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane that finds its segment
 // full then finishes its ray itself (tail_put).  A cap measured slower at every size tried:
 // bunny's passes hand over ~20 % of 128 frames' queued rays (DESIGN Appendix A).
 int tail_stride(int frames, int lanes) {
-    const char* e = getenv("PT_BVH_TAIL_CHUNKS");
+    const int chunks = gp->tune.bvh_tail_chunks;
     const int nb = nblocks(std::max(1, gp->local_pixels * frames));
     const int s = ((nb + NSEG - 1) / NSEG) * (BLOCK / 64) * lanes;
-    return e && atoi(e) > 0 ? std::min(s, atoi(e) * BLOCK) : s;
+    return chunks > 0 ? std::min(s, chunks * BLOCK) : s;
 }
 // paths a pass of `frames` frames needs room for, tile-padded (kernels may read a whole tile)
 int capacity_for(int frames) {
@@ -2035,9 +2112,9 @@ int ensure_frames(int frames) {
         RC(dalloc(&gp->queue.C, qn));
         RC(dalloc(&gp->queue.D, qn));
         gp->tail_lanes = bvh_tail_lanes();
-        gp->tail_refill = getenv("PT_BVH_TAIL_REFILL") ? std::max(1, std::min(64, atoi(getenv("PT_BVH_TAIL_REFILL")))) : 16;
-        gp->tail_trav_blocks = getenv("PT_BVH_TAIL_TRAV_BLOCKS") ? std::max(1, atoi(getenv("PT_BVH_TAIL_TRAV_BLOCKS"))) : 224;
-        gp->tail_shade_blocks = getenv("PT_BVH_TAIL_SHADE_BLOCKS") ? atoi(getenv("PT_BVH_TAIL_SHADE_BLOCKS")) : 512;
+        gp->tail_refill = gp->tune.tail_refill;
+        gp->tail_trav_blocks = gp->tune.tail_trav_blocks;
+        gp->tail_shade_blocks = gp->tune.tail_shade_blocks;
         if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
             gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
             TailBuf& t = gp->tail;
@@ -2305,8 +2382,7 @@ int multi_setup() {
     }
     // tools / tests: PT_COMBINE_FORCE_STAGED=1 sends every PEER shard through its packed tile and a
     // hipMemcpyPeerAsync (the branch taken without peer access), also when the shards share a device
-    const char* fs = getenv("PT_COMBINE_FORCE_STAGED");
-    const bool force_staged = fs && atoi(fs) != 0;
+    const bool force_staged = p->tune.combine_force_staged;
     for (int k = 1; k < M.n; ++k) {
         State* s = M.shard[k];
         const size_t bytes = 3 * sizeof(float) * (size_t)std::max(1, s->local_pixels);
@@ -2540,7 +2616,7 @@ int32_t pt_free(void) {
 // frames per pass when pt_options.frames_per_pass == 0: enough paths in flight to fill the
 // chip in the late, mostly-terminated bounces (~84M paths at bounce 0), at most MAXF
 int auto_batch(int local_pixels) {
-    static const int64_t target = getenv("PT_AUTO_PATHS") ? atoll(getenv("PT_AUTO_PATHS")) : AUTO_BATCH_PATHS;  // tools: A/B
+    const int64_t target = gp->tune.auto_paths > 0 ? gp->tune.auto_paths : AUTO_BATCH_PATHS;
     int f = 1;
     while (f * 2 <= MAXF && (int64_t)local_pixels * f * 2 <= target) f *= 2;
     return f;
@@ -2562,6 +2638,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     HIPCHK(hipSetDevice(o.device));
     gp->opts = o;
     gp->device = o.device;
+    gp->tune = read_tuning();
     HIPCHK(hipStreamCreateWithFlags(&gp->stream, hipStreamNonBlocking));
     gp->width = W;
     gp->height = H;
@@ -2719,7 +2796,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
-    int pair_root_ref = 0, pair_count = 0;
+    int pair_root_ref = 0, pair_count = 0, pair_ref_shift = 16;
 
     float4 pair_root_lo{}, pair_root_hi{};
     double cull_extent = 1.0;
@@ -2874,8 +2951,9 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
         // VAR_BVH_FAST pair layout (DevPair): walk the tree in the reference's visit order
         // (push left, push right, pop -> right subtree first), numbering internal nodes (pairs)
         // and leaves (4-slot triangle groups).  Any tree this layout cannot hold exactly -- a
-        // missing child, a node reached twice, a leaf of more than 4 triangles, more than 65535
-        // refs or a deeper tree than the stack -- keeps the node-array traversal.
+        // missing child, a node reached twice, a leaf of more than 4 triangles, 2^24 refs or more
+        // (pack_ref's widest ref field) or a deeper tree than the stack -- keeps the node-array
+        // traversal.
         {
             const int nn = s->num_bvh_nodes;
             std::vector<int> id(nn, -1);
@@ -2913,7 +2991,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                     fifo.push_back(s->bvh_nodes[n].right);
                 }
             }
-            ok = ok && (int64_t)P + L <= 65535 && height + 1 <= MAXSTACK && !(o.variant & VAR_BVH_NODES);
+            ok = ok && (int64_t)P + L < (1 << 24) && height + 1 <= MAXSTACK && !(o.variant & VAR_BVH_NODES);
             if (ok) {
                 auto ref = [&](int n) { return is_leaf[n] ? P + id[n] : id[n]; };
                 // cull_threshold_packed's constants for a child of cull size s (same c0 and E as
@@ -2943,10 +3021,9 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                 // NaN / infinite bound (the containment argument needs ordered bounds), the union
                 // differs from the reference root box, or the tree would not fit the stack.
                 // PT_BVH_TREE=ref (tools, A/B) keeps the reference's own hierarchy.
-                static const char* tree_env = getenv("PT_BVH_TREE");
                 std::vector<pth::TravInner> tt;
                 int th = 0;
-                bool sah = !(tree_env && strcmp(tree_env, "ref") == 0) && L >= 2;
+                bool sah = !gp->tune.bvh_tree_ref && L >= 2;
                 if (sah) {
                     std::vector<float> llo(3 * (size_t)L), lhi(3 * (size_t)L), ls(L);
                     for (int k = 0; k < L; ++k) {
@@ -2956,7 +3033,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         ls[k] = node_aux[leaf_nodes[k]].y;
                     }
                     sah = pth::build_sah_tree(llo, lhi, ls, tt, th) && th + 1 <= MAXSTACK &&
-                          (int64_t)tt.size() + L <= 65535;
+                          (int64_t)tt.size() + L < (1 << 24);
                     if (sah) {   // the union of the leaves is the reference root box, bit for bit
                         const pth::TravChild& a = tt[0].c[0];
                         const pth::TravChild& b = tt[0].c[1];
@@ -2984,7 +3061,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                     }
                     gp->stack_depth = std::max(gp->stack_depth, th + 1);
                     gp->pair_depth = th + 1;
-                    if (getenv("PT_BVH_TREE_INFO"))
+                    if (gp->tune.bvh_tree_info)
                         fprintf(stderr, "pt_init: SAH traversal tree over %d reference leaves, height %d (reference %d)\n", L,
                                 th, height);
                 }
@@ -3033,6 +3110,10 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                 pair_root_lo = make_float4(nodes[0].lo.x, nodes[0].lo.y, nodes[0].lo.z, 0.f);
                 pair_root_hi = make_float4(nodes[0].hi.x, nodes[0].hi.y, nodes[0].hi.z, node_aux[0].y);
                 pair_count = P;
+                // stack entries: as few ref bits as the P + L refs need, the rest for the cull T
+                int rb = 2;
+                while (((int64_t)1 << rb) < (int64_t)P + L) ++rb;
+                pair_ref_shift = 32 - rb;
             }
         }
         gp->bvh_lds = (size_t)gp->stack_depth * BLOCK * sizeof(int);
@@ -3085,8 +3166,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<unsigned long long> grid;
     float grid_lo[3] = {0.f, 0.f, 0.f}, grid_inv[3] = {0.f, 0.f, 0.f};
     {
-        const char* ge = getenv("PT_GRID");
-        const int grid_env = ge ? atoi(ge) : -1;
+        const int grid_env = gp->tune.grid;
         const int grid_min = grid_env == 1 ? 2 : GRID_MIN_GEOMS;
         if (grid_env != 0 && s->num_geoms >= grid_min && s->num_geoms <= LDS_GEOMS &&
             build_candidate_table(culls, s->num_geoms, s->camera.position, grid, grid_lo, grid_inv)) {
@@ -3174,6 +3254,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.leaf9 = gp->d_leaf9;
     sc.num_pairs = pair_count;
     sc.root_ref = pair_root_ref;
+    sc.ref_shift = pair_ref_shift;
     sc.root_lo = pair_root_lo;
     sc.root_hi = pair_root_hi;
     // node_aux's c = 64 2^-24 sx^2 / 1e-5, stored x 1.01, and cE = c x extent x 1.01: the same
@@ -3275,6 +3356,17 @@ int32_t pt_set_trace_depth(int32_t depth) {
             release_graph();   // the bounce count is baked into the captured passes
         }
     }
+    return PT_OK;
+}
+
+int32_t pt_set_speculation(int32_t enabled) {
+    RC(need_init());
+    State* p = &g_primary;
+    if (!enabled) {
+        ShardScope sc(p);
+        RC(spec_cancel());
+    }
+    p->tune.speculate = enabled != 0;
     return PT_OK;
 }
 
@@ -3393,6 +3485,9 @@ int32_t pt_get_image(float* host_out, int64_t n_floats) {
 
 int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
     RC(need_init());
+    // the caller may write through the pointer before the next pt_trace: a speculated next frame
+    // summed from the image as it is now would then overwrite that write, so it is dropped here
+    RC(spec_cancel());
     HIPCHK(hipStreamSynchronize(gp->stream));
     if (device_ptr) *device_ptr = gp->d_image;
     if (n_floats) *n_floats = (int64_t)gp->pixels_total * 3;
@@ -3452,6 +3547,8 @@ int32_t pt_get_frame_stats(pt_frame_stats* out) {
         for (int b = 0; b <= MAXB; ++b) {
             out->live_total[b] += s.live_total[b];
             out->queued_total[b] += s.queued_total[b];
+            out->handed_total[b] += s.handed_total[b];
+            out->handed_stack_total[b] += s.handed_stack_total[b];
         }
     }
     return PT_OK;
@@ -3485,6 +3582,13 @@ static int32_t frame_stats(pt_frame_stats* out) {
         int64_t q = 0;
         for (int k = 0; k < NSEG; ++k) q += ctl.qcnt[b][k][0];
         out->queued_total[b] = (int64_t)ctl.qtot[b] + (ctl.frames > 0 ? q : 0);
+        int64_t h = 0, hs = 0;
+        for (int k = 0; k < NSEG; ++k) {
+            h += ctl.qcnt[b][k][3];
+            hs += ctl.qcnt[b][k][4];
+        }
+        out->handed_total[b] = (int64_t)ctl.htot[b] + (ctl.frames > 0 ? h : 0);
+        out->handed_stack_total[b] = (int64_t)ctl.hstk[b] + (ctl.frames > 0 ? hs : 0);
         if (b < out->bounces) out->segments_total += out->live_total[b];
     }
     return PT_OK;

@@ -77,7 +77,8 @@ class _FrameStats(ctypes.Structure):
                 ("segments", ctypes.c_int64), ("pixels", ctypes.c_int64), ("frames_total", ctypes.c_int64),
                 ("live_total", ctypes.c_int64 * 65), ("segments_total", ctypes.c_int64),
                 ("frames_per_pass", ctypes.c_int32), ("last_pass_frames", ctypes.c_int32),
-                ("queued_total", ctypes.c_int64 * 65)]
+                ("queued_total", ctypes.c_int64 * 65), ("handed_total", ctypes.c_int64 * 65),
+                ("handed_stack_total", ctypes.c_int64 * 65)]
 
 
 class _KernelTimes(ctypes.Structure):
@@ -97,7 +98,7 @@ ABI_SYMBOLS = [
     "pt_scene_material_name", "pt_scene_free", "pt_scene_last_error", "pt_test_camera", "pt_test_intersect",
     "pt_debug_section_counters", "pt_texture_load",
     "pt_save_png", "pt_scene_load_ex", "pt_bvh_build", "pt_bvh_build_last_error", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
-    "pt_device_alloc", "pt_device_free", "pt_device_read", "pt_set_trace_depth",
+    "pt_device_alloc", "pt_device_free", "pt_device_read", "pt_set_trace_depth", "pt_set_speculation",
 ]
 # include/pt/pt_viewer.h (the headless interactive viewer)
 VIEWER_SYMBOLS = [
@@ -134,7 +135,7 @@ def _load():
         "pt_scene_load_ex": (i32, [ctypes.c_char_p, i32, i32, i32, i32, vp]),
         "pt_bvh_build": (i32, [vp, i32, vp, i32, vp, vp]),
         "pt_bvh_build_last_error": (ctypes.c_char_p, []),
-        "pt_set_trace_depth": (i32, [i32]),
+        "pt_set_trace_depth": (i32, [i32]), "pt_set_speculation": (i32, [i32]),
         "pt_device_alloc": (i32, [i64, vp]), "pt_device_free": (i32, [vp]), "pt_device_read": (i32, [vp, vp, i64]),
         "pt_viewer_create": (i32, [vp, vp, ctypes.c_char_p, ctypes.c_char_p, vp]), "pt_viewer_destroy": (None, [vp]),
         "pt_viewer_mouse_button": (i32, [vp, i32, i32, i32]),
@@ -333,6 +334,10 @@ class PathTracer:
         _check(lib.pt_set_trace_depth(int(depth)), "pt_set_trace_depth")
         self.trace_depth = int(depth)
 
+    def set_speculation(self, enabled: bool):
+        """Next-frame speculation of single-frame calls that copy the image out (default on)."""
+        _check(lib.pt_set_speculation(int(bool(enabled))), "pt_set_speculation")
+
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")
         self.iteration = first_iteration + count - 1
@@ -366,7 +371,9 @@ class PathTracer:
                 "live_total": [s.live_total[i] for i in range(s.bounces + 1)],
                 "segments_total": s.segments_total, "frames_per_pass": s.frames_per_pass,
                 "last_pass_frames": s.last_pass_frames,
-                "queued_total": [s.queued_total[i] for i in range(s.bounces + 1)]}
+                "queued_total": [s.queued_total[i] for i in range(s.bounces + 1)],
+                "handed_total": [s.handed_total[i] for i in range(s.bounces + 1)],
+                "handed_stack_total": [s.handed_stack_total[i] for i in range(s.bounces + 1)]}
 
     def reset_stats(self):
         _check(lib.pt_reset_stats(), "pt_reset_stats")

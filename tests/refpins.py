@@ -176,7 +176,8 @@ def scene_targets(geoms: np.ndarray, triangles: np.ndarray) -> np.ndarray:
 # scenes whose intersections are pinned (primitives only / meshes with the synthetic stand-ins)
 ISECT_SCENES = ["cornell", "cornell_glass_test", "cornell_microfacet_test", "cornell_reflective_test",
                 "cornell_transmissive_test", "cornell_multiple_glass", "sphere", "cornell_obj_bnnuy",
-                "cornell_obj_khaslana", "cornell_obj_phatphuck_texture_test", "cornell_obj_phainon_halo"]
+                "cornell_obj_khaslana", "cornell_obj_phatphuck_texture_test", "cornell_obj_phainon_halo",
+                "cornell_obj_cyrene", "cornell_obj_phainon"]   # 262k / 1.0M-triangle stand-ins
 ISECT_RAYS = 4096
 
 

@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol(ptamd):
 
 
 def test_version_and_defaults(ptamd):
-    assert ptamd.lib.pt_abi_version() == 2
+    assert ptamd.lib.pt_abi_version() == 3
     o = ptamd.default_options()
     # the reference's compile-time defaults, pathtrace.cu:20-24
     assert (o.stream_compaction, o.material_sort, o.bvh) == (1, 0, 1)

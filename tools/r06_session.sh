@@ -1,0 +1,65 @@
+#!/usr/bin/env bash
+# Round-6 GPU session: tools/r06_session.sh STEP...
+# Each step has its own time limit; a failure other than test failures stops the session.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {   # step NAME TIMEOUT CMD...
+    local name=$1 to=$2; shift 2
+    echo "== $name (timeout ${to}s) =="
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    tail -n 5 "$OUT/$name.log"
+    echo "== $name rc=$rc =="
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name rc=$rc"; exit $rc; fi
+    return 0
+}
+PYT="python -u -m pytest -x -q -rf --timeout 200 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+    case $s in
+        new) step pytest_new 500 $PYT tests/test_multi_device.py tests/test_dropin.py -m gpu ;;
+        spec) step pytest_spec 300 $PYT tests/test_speculation.py -m gpu ;;
+        glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
+        meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
+        mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
+        gpu) step pytest_gpu 900 $PYT tests -m gpu ;;
+        smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) step bench_k20 400 python bench.py --steps 20 --warmup 5 ;;
+        benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
+        multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
+        multidirect) PT_MULTI_F1_DIRECT=1 step multi_probe_direct 300 python tools/multi_probe.py 20 ;;
+        inproc) step inproc 200 python bench.py --gpus 2 --inproc --inproc-devices 0,0 --steps 20 --warmup 5 ;;
+        ab_*)   # ab_<tag>: AB_LIBS / AB_ROUNDS from the environment, scenes below
+            tag=${s#ab_}
+            B=project3-cuda-path-tracer-2025_amd/build/ab
+            [ -z "${AB_SKIP_CORNELL:-}" ] && AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
+            AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
+            AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
+        profiles) step profiles 1100 bash tools/r05_profiles.sh ;;
+        apicopy)
+            step prof_api_copy 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/prof_api_copy -o run --output-format csv -- python tools/api_trace.py run copy
+            python tools/api_trace.py overlap gpurun_out/prof_api_copy/run_kernel_trace.csv gpurun_out/prof_api_copy/run_memory_copy_trace.csv --out gpurun_out/api_copy_overlap.json ;;
+        benchapi) step bench_api 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-configs --no-spread ;;
+        hist) step sec_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_bunny.json
+            step sec_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana.json ;;
+        large) step pytest_large 600 $PYT tests/test_large_mesh.py -m gpu ;;
+        benchlarge) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
+            step bench_cyrene 300 $B --steps 24 --warmup 2 --scene scenes/cornell_obj_cyrene.json
+            step bench_cyrene_nodes 300 $B --steps 8 --warmup 1 --scene scenes/cornell_obj_cyrene.json --variant 250
+            step bench_phainon 300 $B --steps 24 --warmup 2 --scene scenes/cornell_obj_phainon.json
+            step bench_phainon_nodes 300 $B --steps 8 --warmup 1 --scene scenes/cornell_obj_phainon.json --variant 250 ;;
+        tailtest) step pytest_tail 400 $PYT tests/test_bvh_tail.py -m gpu ;;
+        meshlanes) PT_BVH_TAIL_LANES=${MESH_TAIL:-16} step pytest_meshlanes 600 $PYT tests/test_gpu_parity.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or config5 or speculated" ;;
+        laneab) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=0 PT_BVH_TAIL_LANES=16 PT_BVH_TAIL_LANES=24 PT_BVH_TAIL_LANES=32}"
+            AB_TAG=lane_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lane_bunny 900 bash tools/ab_env.sh
+            AB_TAG=lane_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_lane_khaslana 900 bash tools/ab_env.sh ;;
+        meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
+            step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
+            step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "session done"
