@@ -219,7 +219,13 @@ def main():
     # RCCL (backend "nccl") in production; PT_BENCH_BACKEND=gloo rehearses the multi-rank logic
     # with several ranks sharing one GPU (the framebuffer combine then goes through host memory)
     backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
-    device = local % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and world > n_dev:
+        # one rank per GPU: RCCL ranks stacked on one device would time a different job
+        print(f"bench.py: {world} RCCL ranks but {n_dev} visible GPUs (PT_BENCH_BACKEND=gloo rehearses "
+              "ranks that share a GPU)", file=sys.stderr)
+        sys.exit(2)
+    device = local % max(1, n_dev)
     if world > 1:
         torch.cuda.set_device(device)
         if backend == "nccl":
@@ -414,6 +420,7 @@ def sub_config(ptamd, cfg):
                                               "c5_khaslana" if "khaslana" in scene_name and res == (1600, 1600)
                                               and depth == 12 else
                                               "staged_c2" if pipeline == "staged" and "glass" in scene_name and sort
+                                              else "m262k_cyrene" if "cyrene" in scene_name and not opts
                                               else None)),
            "kernels": kernels_digest(prof, None)}
     if "obj" in scene_name:

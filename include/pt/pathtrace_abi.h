@@ -292,8 +292,13 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
  * traversal iterations by active lanes in bins of 4 (1-4, 5-8, ..), [36..51] the same for the
  * handed-over traversals' kernel, [52..67] handed-over rays by stack depth (8 buckets: count,
  * nodes visited after), [68..71] by a hit found before (no: count, nodes; yes: count, nodes);
- * n <= 76.  `reset` zeroes them after the read. */
+ * [72] candidate-table pre-test superset sizes over the live lanes, [73] the sum over waves of
+ * each wave's largest superset; n <= 76.  `reset` zeroes them after the read. */
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset);
+
+/* Next-frame speculation (pt_set_speculation): frames speculated and frames taken over since
+ * pt_init, summed over the context's shards (either pointer may be NULL).  Tests and tools. */
+int32_t pt_debug_spec_counts(int64_t* launched, int64_t* adopted);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,7 @@ struct SceneDev {
     const unsigned long long* grid;
     unsigned long long grid_all;   // every geom (rays outside the table's domain)
     float grid_lo[3], grid_inv[3]; // cell = floor((o - grid_lo) * grid_inv), GRID_G per axis
+    int sort_next;                 // k_bounce orders its survivors by their next superset's size (grid != null)
 };
 
 // The candidate table's resolution: GRID_G^3 origin cells x 6 faces x GRID_B^2 direction bins
@@ -126,7 +127,9 @@ enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EX
        SEC_TAIL_BY_SP = SEC_TAIL_LANES_HIST + 16,   // handed-over rays by stack depth at the hand-over
                                                     // (0, 1, 2, 3, 4-5, 6-7, 8-11, 12+): count, nodes after
        SEC_TAIL_BY_HIT = SEC_TAIL_BY_SP + 16,       // ... by "a hit found before": no (count, nodes), yes
-       SEC_COUNT = SEC_TAIL_BY_HIT + 4 };
+       SEC_N_SUP = SEC_TAIL_BY_HIT + 4,             // candidate table: superset sizes over the live lanes
+       SEC_N_SUP_WMAX,                              // ... and the sum over waves of the wave's largest
+       SEC_COUNT };
 constexpr int SEC_SLOTS = 76;
 __device__ unsigned long long g_sections[SEC_SLOTS];
 PT_DEV uint64_t sec_clock() { return __builtin_amdgcn_s_memtime(); }
@@ -1345,6 +1348,13 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
                                               bounded)
                        : cull_candidates(sc, lg, cr, ro, rd, bounded);
         PT_HOOK(DUP_CULL, sc, lg, ro, rd, bounded);
+    }
+    if (TIMING && sc.grid) {   // the per-lane superset loop costs a wave its largest superset
+        int ss = live ? __popcll(grid_superset(sc, ro, rd)) : 0;
+        sec_add_lanes(SEC_N_SUP, ss);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) ss = max(ss, __shfl_xor(ss, off, 64));
+        sec_add(SEC_N_SUP_WMAX, (uint64_t)ss);
     }
     const int cnt = __builtin_popcountll(cand);
     uint64_t tc1 = 0;

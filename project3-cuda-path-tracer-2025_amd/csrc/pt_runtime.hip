@@ -314,6 +314,59 @@ PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i
     i1 = TWO ? s_b[1] + s_w[1][w] + mbcnt(m1) : 0;
 }
 
+// block_append for flag 0 with its survivors ordered by a key (0..15) within the block's output
+// chunk: (key, wave, lane) order, so that the next bounce's waves -- which take consecutive paths
+// -- hold paths of like key.  Same atomics as block_append (one per counter per block), no extra
+// barrier: each wave's lanes 0..15 count their key among the wave's flagged lanes from four
+// ballots, wave 0 scans the 64 (key, wave) counts.  `sk`: 70 ints of LDS that no thread reads
+// after the caller's last barrier.  Every thread of the block must call it.
+template <bool TWO>
+PT_DEV void block_append_keyed(bool f0, int key, int* ctr0, bool f1, int* ctr1, int& i0, int& i1, int* sk) {
+    int* s_k = sk;            // [wave][key] counts, then the (key, wave) exclusive offsets
+    int* s_w1 = sk + 64;      // flag 1 per wave
+    int* s_b = sk + 68;       // the two atomics' bases
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t m0 = __ballot(f0);
+    uint64_t bb[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bb[b] = __ballot(f0 && ((key >> b) & 1));
+    const uint64_t m1 = TWO ? __ballot(f1) : 0ull;
+    auto peers = [&](int k) {
+        uint64_t m = m0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) m &= ((k >> b) & 1) ? bb[b] : ~bb[b];
+        return m;
+    };
+    if (lane < 16) s_k[w * 16 + lane] = __popcll(peers(lane));
+    if (TWO && lane == 0) s_w1[w] = __popcll(m1);
+    __syncthreads();
+    if (w == 0) {   // entry lane = key * 4 + wave, in that order
+        const int k = lane >> 2, ww = lane & 3;
+        const int v = s_k[ww * 16 + k];
+        int incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const int tot = __shfl(incl, 63, 64);
+        s_k[ww * 16 + k] = incl - v;
+        if (lane == 0) s_b[0] = tot ? atomicAdd(ctr0, tot) : 0;
+    } else if (TWO && tid == 64) {
+        int tot = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) {
+            const int c = s_w1[i];
+            s_w1[i] = tot;
+            tot += c;
+        }
+        s_b[1] = tot ? atomicAdd(ctr1, tot) : 0;
+    }
+    __syncthreads();
+    i0 = f0 ? s_b[0] + s_k[w * 16 + key] + mbcnt(peers(key)) : 0;
+    i1 = TWO ? s_b[1] + s_w1[w] + mbcnt(m1) : 0;
+}
+
 template <bool FIRST, bool HAS_BVH, int VAR>
 __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride,
@@ -457,7 +510,20 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     }
     // block-aggregated compaction (+ the traversal queue): one atomic per counter per block
     int si, qi;
-    block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
+    // candidate-table scenes (SceneDev::sort_next): survivors ordered in the block's chunk by the
+    // size of their next pre-test superset, so that the next bounce's per-lane superset loop
+    // (cull_candidates_grid, which costs a wave its largest superset) meets like sizes in a wave.
+    // The exchange's ray rows are free here: their readers all precede block_intersect's last barrier.
+    // (mesh kernels only: the reference's candidate-table scenes are mesh scenes, and the
+    // primitive-only kernels keep their scalar registers)
+    constexpr bool KEYED = HAS_BVH && REDIST && (VAR & VAR_BLOCK_REDIST) && !MG;
+    if (KEYED && sc.sort_next && lds_geoms) {
+        const int key = surv ? min(15, __popcll(grid_superset(sc, p.o, p.d))) : 0;
+        block_append_keyed<SPLIT>(surv, key, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si,
+                                  qi, reinterpret_cast<int*>(reinterpret_cast<BlockLds*>(s_wave_isect - (tid >> 6))->ro[0]));
+    } else {
+        block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
+    }
     if (surv) store_path(out, seg * seg_stride + si, p);
     qi += seg * q.stride;
     if (SPLIT && queued) queue_put(q, qi, p, qt, qw, qs);
@@ -722,6 +788,111 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
         }
     }
 }
+// k_bvh_tail_trav with the shading folded in (PT_BVH_TAIL_FUSED=1): a finished ray is not written
+// back for k_bvh_tail_shade but waits in its lane; whenever the wave would refill (or has nothing
+// left to traverse), its finished lanes are shaded together -- the queue entry's other words, the
+// hit, shade_path, the gather of a terminated path -- and the survivors appended to the output
+// segment with one atomic per wave.  Saves the final hit's write and read, the entry's re-read of
+// slot and hit, and k_bvh_tail_shade's launch; the shading runs at the refill's lane count.
+#ifndef TAIL_FUSED_WAVES
+#define TAIL_FUSED_WAVES 6
+#endif
+template <int VAR>
+__global__ __launch_bounds__(BLOCK, TAIL_FUSED_WAVES) void k_bvh_tail_fused(SceneDev sc, QueueBuf q, TailBuf t, PathBuf out,
+                                                                     FrameCtl* ctl, float* __restrict__ image,
+                                                                     int bounce, int refill, int seg_stride) {
+    extern __shared__ float4 s_dyn[];
+    int* s_stack = reinterpret_cast<int*>(s_dyn) + threadIdx.x;
+    const int seg = blockIdx.x & (NSEG - 1);
+    const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
+    if (n == 0) return;
+    const int iter = ctl->iter;
+    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;
+    const int lane = threadIdx.x & 63;
+    int next = 0;   // the segment's next untaken entry, as of this wave's last refill
+    constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
+    int e = -1, qs = 0, n_nodes = 0, n_tris = 0, sp0 = 0;
+    bool hit0 = false;
+    TravState st;
+    st.cur = -1;
+    while (true) {
+        const bool fin = e >= 0 && st.cur < 0;              // traversed, not yet shaded
+        const uint64_t free_m = __ballot(e < 0 || fin);
+        const int n_free = __popcll(free_m);
+        const bool more = next < n;
+        if (n_free >= refill || n_free == 64) {   // (64: nothing is traversing)
+            if (__ballot(fin) != 0) {   // shade the finished lanes together
+                PathReg p;
+                p.rb = 0;
+                if (fin) {
+                    p.o = st.ro;
+                    p.d = st.rd;
+                    bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
+                }
+                const bool surv = fin && p.rb > 0;
+                if (fin && !surv) gather_into_image(image, sc, to_plane, p);
+                const uint64_t m = __ballot(surv);
+                if (m != 0) {
+                    const int lead = __builtin_ctzll(m);
+                    int base = 0;
+                    if (lane == lead) base = atomicAdd(&ctl->cnt[bounce + 1][seg][0], __popcll(m));
+                    base = __builtin_amdgcn_readlane(base, lead);
+                    if (surv) store_path(out, seg * seg_stride + base + mbcnt(m), p);
+                }
+                if (fin) e = -1;
+            }
+            if (more) {
+                const uint64_t idle = __ballot(e < 0);
+                const int n_idle = __popcll(idle);
+                const int lead = __builtin_ctzll(idle);
+                int b0 = 0;
+                if (lane == lead) b0 = atomicAdd(&ctl->qcnt[bounce][seg][2], n_idle);
+                next = __builtin_amdgcn_readlane(b0, lead);
+                if (e < 0) {
+                    const int k = next + mbcnt(idle);
+                    if (k < n) {
+                        e = seg * t.stride + k;
+                        const int2 nd = t.node[e];
+                        qs = nd.x;
+                        const float4 a = q.A[qs], b = q.B[qs];
+                        trav_resume(st, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), t.hit[e], nd.y);
+                        for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK] = t.stack[(size_t)i * t.cap + e];
+                        n_nodes = n_tris = 0;
+                        if (CNT) {
+                            sp0 = st.sp;
+                            hit0 = st.btri != 0x7fffffff;
+                        }
+                    }
+                }
+                next += n_idle;
+            }
+        }
+        const bool trav = e >= 0 && st.cur >= 0;
+        const int lanes = __popcll(__ballot(trav));
+        if (lanes == 0) {
+            if (__ballot(e >= 0) == 0 && next >= n) break;   // nothing left to shade or take
+            continue;
+        }
+        if (trav) {
+            if (CNT) {
+                sec_add(SEC_N_BVH_WITERS, 1);
+                sec_add(SEC_TAIL_LANES_HIST + (lanes - 1) / 4, 1);
+            }
+            trav_step<CNT>(sc, st, s_stack, n_nodes, n_tris);
+            if (CNT && st.cur < 0) {
+                sec_add_lanes(SEC_N_NODES, n_nodes);
+                sec_add_lanes(SEC_N_TRIS, n_tris);
+                bvh_count_ray<CNT>(st, q.D[qs].x, n_nodes);
+                const int bk = sp0 < 4 ? sp0 : sp0 < 6 ? 4 : sp0 < 8 ? 5 : sp0 < 12 ? 6 : 7;
+                sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk, 1);
+                sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk + 1, n_nodes);
+                sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 2 : 0), 1);
+                sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 3 : 1), n_nodes);
+            }
+        }
+    }
+}
+
 // ... and their shading, gather and compaction, as k_bvh_bounce's: block b takes the chunks
 // j = b / NSEG, + gridDim / NSEG, .. of BLOCK entries of segment s = b % NSEG, survivors to output
 // segment s (a grid for the usual counts, not for the capacity: empty blocks cost dispatch time)
@@ -1152,6 +1323,8 @@ struct Tuning {
     int tail_refill = 16;                           // PT_BVH_TAIL_REFILL (1..64 idle lanes)
     int tail_trav_blocks = 224;                     // PT_BVH_TAIL_TRAV_BLOCKS per segment
     int tail_shade_blocks = 512;                    // PT_BVH_TAIL_SHADE_BLOCKS per segment (0: one per chunk)
+    bool sort_next = false;                         // PT_SORT_NEXT=1: SceneDev::sort_next (candidate-table scenes)
+    bool tail_fused = false;                        // PT_BVH_TAIL_FUSED=1: k_bvh_tail_fused (shading in the refilling waves)
     bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
     bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
@@ -1178,6 +1351,8 @@ Tuning read_tuning() {
     t.tail_refill = (int)std::max(1L, std::min(64L, num("PT_BVH_TAIL_REFILL", 16)));
     t.tail_trav_blocks = (int)std::max(1L, num("PT_BVH_TAIL_TRAV_BLOCKS", 224));
     t.tail_shade_blocks = (int)std::max(0L, num("PT_BVH_TAIL_SHADE_BLOCKS", 512));
+    t.tail_fused = num("PT_BVH_TAIL_FUSED", 0) != 0;
+    t.sort_next = num("PT_SORT_NEXT", 0) != 0;
     t.combine_force_staged = num("PT_COMBINE_FORCE_STAGED", 0) != 0;
     const char* tree = getenv("PT_BVH_TREE");
     t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
@@ -1262,6 +1437,7 @@ struct State {
     hipGraph_t spec_graph = nullptr;      // its pass, captured once (released with the pass graphs)
     hipGraphExec_t spec_exec = nullptr;
     int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
+    int64_t spec_launched = 0, spec_adopted = 0;   // speculated frames queued / taken over (pt_debug_spec_counts)
     int spec_dev_iter = 0;                // d_ctl_spec->iter after the speculative frames queued so far
     int key_bits = 1;
     bool multi = false;              // a shard context of a multi-device pt_init
@@ -1383,7 +1559,10 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
         if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
         launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail,
                gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
-        if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
+        if (gp->tail_lanes > 0 && gp->tune.tail_fused) {   // refilling waves that shade what they finish
+            launch(400 + b, k_bvh_tail_fused<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
+                   gp->queue, gp->tail, out, gp->d_ctl, gp->d_image, b, gp->tail_refill, gp->seg_stride);
+        } else if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
             launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
                    gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
             const int per_seg = gp->tail_shade_blocks > 0 ? std::min(gp->tail_shade_blocks, nblocks(gp->tail.stride))
@@ -1640,73 +1819,73 @@ int run_frame(int iter) { return run_pass(iter, 1); }
 // copy by as much.  The caller records spec_ev_in, hands the launcher {stream, graph, events,
 // iteration preset} and goes straight on to the copy; everything that later touches the speculative
 // stream, its events or its graph waits for the launcher first (spec_worker_idle).
+// One launch: {device, stream, events, graph, iteration preset, k_spec_sum's buffers}.  A call of a
+// context of several devices posts one per shard together; the launcher queues them in order.
+struct SpecTask {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_done = nullptr;
+    hipGraphExec_t exec = nullptr;
+    int* iter_ptr = nullptr;
+    int preset = -1;                 // < 0: the iteration is already right
+    const float* image = nullptr;    // k_spec_sum: image + plane -> sum
+    const float* plane = nullptr;
+    float* sum = nullptr;
+    int nf = 0;
+};
+// Threading: the launcher thread only ever touches the HIP objects of the tasks handed to it (by
+// value) and its own current device (hipSetDevice is per host thread); it never reads the
+// runtime's process-global context (gp, M) nor calls RCCL.  The caller waits for it (idle) before
+// it touches a posted task's stream, events or graph again.
 struct SpecLauncher {
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
     bool task = false, busy = false, stop = false;
     hipError_t err = hipSuccess;
-    // the task
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev_in = nullptr, ev_done = nullptr;
-    hipGraphExec_t exec = nullptr;
-    int* iter_ptr = nullptr;
-    int preset = -1;   // < 0: the iteration is already right
-    const float* image = nullptr;   // k_spec_sum: image + plane -> sum
-    const float* plane = nullptr;
-    float* sum = nullptr;
-    int nf = 0;
+    SpecTask tasks[PT_MAX_DEVICES];
+    int ntasks = 0;
 
+    static hipError_t launch_one(const SpecTask& t) {
+        hipError_t e = hipSetDevice(t.device);
+        if (e == hipSuccess) e = hipStreamWaitEvent(t.stream, t.ev_in, 0);
+        if (e == hipSuccess && t.preset >= 0) e = hipMemsetD32Async((hipDeviceptr_t)t.iter_ptr, t.preset, 1, t.stream);
+        if (e == hipSuccess) e = hipGraphLaunch(t.exec, t.stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_spec_sum, dim3(nblocks((t.nf + 3) / 4)), dim3(BLOCK), 0, t.stream, t.image, t.plane,
+                               t.sum, t.nf);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(t.ev_done, t.stream);
+        return e;
+    }
     void run() {
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             cv.wait(lk, [&] { return task || stop; });
             if (stop) return;
             task = false;
-            const int dev = device, pre = preset;
-            hipStream_t st = stream;
-            hipEvent_t ei = ev_in, ed = ev_done;
-            hipGraphExec_t ex = exec;
-            int* ip = iter_ptr;
-            const float *im = image, *pl = plane;
-            float* su = sum;
-            const int n = nf;
+            SpecTask ts[PT_MAX_DEVICES];
+            const int n = ntasks;
+            for (int i = 0; i < n; ++i) ts[i] = tasks[i];
             lk.unlock();
-            hipError_t e = hipSetDevice(dev);
-            if (e == hipSuccess) e = hipStreamWaitEvent(st, ei, 0);
-            if (e == hipSuccess && pre >= 0) e = hipMemsetD32Async((hipDeviceptr_t)ip, pre, 1, st);
-            if (e == hipSuccess) e = hipGraphLaunch(ex, st);
-            if (e == hipSuccess) {
-                hipLaunchKernelGGL(k_spec_sum, dim3(nblocks((n + 3) / 4)), dim3(BLOCK), 0, st, im, pl, su, n);
-                e = hipGetLastError();
-            }
-            if (e == hipSuccess) e = hipEventRecord(ed, st);
+            hipError_t e = hipSuccess;
+            for (int i = 0; i < n && e == hipSuccess; ++i) e = launch_one(ts[i]);
             lk.lock();
             if (e != hipSuccess) err = e;
             busy = false;
             cv.notify_all();
         }
     }
-    void post(int dev, hipStream_t st, hipEvent_t ei, hipEvent_t ed, hipGraphExec_t ex, int* ip, int pre,
-              const float* im, const float* pl, float* su, int n) {
+    void post(const SpecTask* t, int n) {
         std::lock_guard<std::mutex> lk(mu);
         if (!th.joinable()) th = std::thread([this] { run(); });
-        device = dev;
-        stream = st;
-        ev_in = ei;
-        ev_done = ed;
-        exec = ex;
-        iter_ptr = ip;
-        preset = pre;
-        image = im;
-        plane = pl;
-        sum = su;
-        nf = n;
+        for (int i = 0; i < n; ++i) tasks[i] = t[i];
+        ntasks = n;
         task = busy = true;
         cv.notify_all();
     }
-    hipError_t idle() {   // wait until the posted launch is queued; its error, once
+    hipError_t idle() {   // wait until the posted launches are queued; their error, once
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return !busy; });
         const hipError_t e = err;
@@ -1730,9 +1909,11 @@ int spec_worker_idle() {
     return PT_OK;
 }
 
+// the calling context (g_primary): one device context, or the shards of a multi-device one (each
+// speculates its own pixels); not a pixel shard of a one-process-per-GPU job (its caller combines)
 bool spec_enabled() {
-    return gp->tune.speculate && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED &&
-           gp->sc.shard.mode != PT_SHARD_PIXELS;
+    return g_primary.tune.speculate && gp == &g_primary && gp->opts.pipeline == PT_PIPELINE_FUSED &&
+           (gp->multi || gp->sc.shard.mode != PT_SHARD_PIXELS);
 }
 int spec_cancel() {
     if (gp->spec_iter == 0) return PT_OK;
@@ -1772,8 +1953,9 @@ void spec_release() {
     gp->spec_iter = 0;
     gp->spec_dev_iter = 0;
 }
-// queue frame `iter` on the speculation stream, behind everything queued on gp->stream so far
-int spec_launch(int iter) {
+// frame `iter` of the current context on its speculation stream, behind everything queued on
+// gp->stream so far: the launch is described in `t` (posted by the caller, with the other shards')
+int spec_prepare(int iter, SpecTask& t) {
     if (!gp->spec_stream) {
         HIPCHK(hipStreamCreateWithFlags(&gp->spec_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&gp->spec_ev_in, hipEventDisableTiming));
@@ -1784,7 +1966,6 @@ int spec_launch(int iter) {
         for (float*& p : gp->d_spec_sum) HIPCHK(hipMalloc((void**)&p, sizeof(float) * 3 * (size_t)gp->pixels_total));
         HIPCHK(hipStreamCreateWithFlags(&gp->copy_stream, hipStreamNonBlocking));
     }
-    RC(spec_worker_idle());   // the launcher is done with the previous launch (events, graph)
     if (!gp->spec_exec) {   // captured once (released with the pass graphs: camera, depth, buffers)
         hipStream_t main_stream = gp->stream;
         FrameCtl* main_ctl = gp->d_ctl;
@@ -1810,11 +1991,20 @@ int spec_launch(int iter) {
     // not iter - 1 (consecutive calls launch the graph alone)
     HIPCHK(hipEventRecord(gp->spec_ev_in, gp->stream));
     gp->spec_sum_idx ^= 1;   // the other buffer: the one the caller may still be copying from is kept
-    g_spec_launcher.post(gp->device, gp->spec_stream, gp->spec_ev_in, gp->spec_ev_done, gp->spec_exec,
-                         &gp->d_ctl_spec->iter, gp->spec_dev_iter != iter - 1 ? iter - 1 : -1, gp->d_image,
-                         gp->d_spec_plane, gp->d_spec_sum[gp->spec_sum_idx], 3 * gp->pixels_total);
+    t.device = gp->device;
+    t.stream = gp->spec_stream;
+    t.ev_in = gp->spec_ev_in;
+    t.ev_done = gp->spec_ev_done;
+    t.exec = gp->spec_exec;
+    t.iter_ptr = &gp->d_ctl_spec->iter;
+    t.preset = gp->spec_dev_iter != iter - 1 ? iter - 1 : -1;
+    t.image = gp->d_image;
+    t.plane = gp->d_spec_plane;
+    t.sum = gp->d_spec_sum[gp->spec_sum_idx];
+    t.nf = 3 * gp->pixels_total;
     gp->spec_dev_iter = iter;
     gp->spec_iter = iter;
+    gp->spec_launched += 1;
     return PT_OK;
 }
 // the call for the speculative frame's iteration: take it over on gp->stream
@@ -1838,6 +2028,7 @@ int spec_adopt(bool copy_out) {
     gp->dev_iter = iter;
     gp->last_iter = iter;
     gp->frames_done += 1;
+    gp->spec_adopted += 1;
     return PT_OK;
 }
 
@@ -2339,6 +2530,25 @@ struct ShardScope {
     }
 };
 
+// frame `iter` speculated by every shard of the calling context, as one post to the launcher
+int spec_launch(int iter) {
+    RC(spec_worker_idle());   // the launcher is done with the previous launches (events, graphs)
+    SpecTask ts[PT_MAX_DEVICES];
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        RC(spec_prepare(iter, ts[k]));
+    }
+    g_spec_launcher.post(ts, nshards());
+    return PT_OK;
+}
+// every shard's speculated frame waited for and dropped
+int spec_cancel_all() {
+    for (int k = 0; k < nshards(); ++k) {
+        ShardScope sc(shard_ctx(k));
+        RC(spec_cancel());
+    }
+    return PT_OK;
+}
 int need_single(const char* what) {
     if (M.n > 1) return fail(PT_E_UNSUPPORTED, "%s: one device context only (pt_options.num_devices > 1)", what);
     return spec_cancel();   // the test / profiling entry points use the path buffers themselves
@@ -3262,6 +3472,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
     sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
     sc.grid = gp->d_grid;
+    sc.sort_next = gp->d_grid && gp->tune.sort_next ? 1 : 0;
     sc.grid_all = s->num_geoms >= 64 ? ~0ull : ((1ull << s->num_geoms) - 1);
     for (int a = 0; a < 3; ++a) {
         sc.grid_lo[a] = grid_lo[a];
@@ -3359,13 +3570,22 @@ int32_t pt_set_trace_depth(int32_t depth) {
     return PT_OK;
 }
 
+int32_t pt_debug_spec_counts(int64_t* launched, int64_t* adopted) {
+    RC(need_init());
+    int64_t l = 0, a = 0;
+    for (int k = 0; k < nshards(); ++k) {
+        l += shard_ctx(k)->spec_launched;
+        a += shard_ctx(k)->spec_adopted;
+    }
+    if (launched) *launched = l;
+    if (adopted) *adopted = a;
+    return PT_OK;
+}
+
 int32_t pt_set_speculation(int32_t enabled) {
     RC(need_init());
     State* p = &g_primary;
-    if (!enabled) {
-        ShardScope sc(p);
-        RC(spec_cancel());
-    }
+    if (!enabled) RC(spec_cancel_all());
     p->tune.speculate = enabled != 0;
     return PT_OK;
 }
@@ -3375,15 +3595,18 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     RC(need_init());
     if (iteration <= 0) return fail(PT_E_INVALID, "iteration is 1-based (main.cpp:458), got %d", iteration);
     // speculate only for callers that copy the image out (main.cpp's pathtrace() always does): a
-    // call without the copy has nothing for the next frame to overlap with
-    const bool spec = M.n <= 1 && spec_enabled() && (host_image != nullptr || gp->spec_iter == iteration);
+    // call without the copy has nothing for the next frame to overlap with.  Several devices: every
+    // shard speculates its own pixels; the call for N + 1 takes each shard's frame over, then
+    // combines as usual (the host copy reads the combined image, so it waits for the combine)
+    const bool spec = spec_enabled() && (host_image != nullptr || gp->spec_iter == iteration);
+    const bool single = M.n <= 1;
     bool adopted = false;
     const int sum_idx = gp->spec_sum_idx;   // the taken-over frame's image, before the next launch flips it
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (spec && gp->spec_iter == iteration) {
             adopted = true;
-            RC(spec_adopt(host_image != nullptr));   // traced already, during the previous call's copy
+            RC(spec_adopt(host_image != nullptr && single));   // traced already, during the previous call's copy
         } else {
             RC(spec_cancel());
             RC(run_frame(iteration));
@@ -3405,7 +3628,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
         // one at the same address, and on MI355X the pageable copy runs at the pinned rate anyway
         // (tools/copy_probe.py: 7.68 MB in 0.145 ms either way)
         const size_t bytes = sizeof(float) * 3 * (size_t)gp->pixels_total;
-        if (adopted)   // the speculated frame's finished sum, on the copy stream (it waited for it)
+        if (adopted && single)   // the speculated frame's finished sum, on the copy stream (it waited for it)
             HIPCHK(hipMemcpyAsync(host_image, gp->d_spec_sum[sum_idx], bytes, hipMemcpyDeviceToHost, gp->copy_stream));
         else
             HIPCHK(hipMemcpyAsync(host_image, gp->d_image, bytes, hipMemcpyDeviceToHost, gp->stream));
@@ -3413,7 +3636,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     // one wait: the first device's stream waited for every shard's frame (multi_combine), and each
     // shard queued its counter copy before that
     HIPCHK(hipStreamSynchronize(gp->stream));
-    if (adopted && host_image) HIPCHK(hipStreamSynchronize(gp->copy_stream));
+    if (adopted && single && host_image) HIPCHK(hipStreamSynchronize(gp->copy_stream));
     if (gp->traced_depth) {
         // GuiDataContainer::TracedDepth = the bounces the frame ran (pathtrace.cu:759-770); with
         // shards, the frame ran as long as its longest shard
@@ -3429,7 +3652,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
 
 int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
     RC(need_init());
-    RC(spec_cancel());
+    RC(spec_cancel_all());
     if (first_iteration <= 0 || count < 0) return fail(PT_E_INVALID, "bad iteration range");
     // passes of gp->batch frames (bit-identical to frame-by-frame: k_combine keeps the order);
     // every shard's passes are queued before the combine, so the devices trace concurrently
@@ -3446,7 +3669,7 @@ int32_t pt_trace_frames(int32_t first_iteration, int32_t count) {
 
 int32_t pt_prepare_frames(int32_t count) {
     RC(need_init());
-    RC(spec_cancel());
+    RC(spec_cancel_all());
     if (count < 0) return fail(PT_E_INVALID, "bad count");
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
@@ -3464,9 +3687,12 @@ int32_t pt_prepare_frames(int32_t count) {
 
 int32_t pt_synchronize(void) {
     RC(need_init());
-    if (g_primary.spec_stream) {   // it stays valid
-        HIPCHK(g_spec_launcher.idle());
-        HIPCHK(hipStreamSynchronize(g_primary.spec_stream));
+    HIPCHK(g_spec_launcher.idle());
+    for (int k = 0; k < nshards(); ++k) {   // speculated frames (their streams stay valid)
+        State* s = shard_ctx(k);
+        if (!s->spec_stream) continue;
+        ShardScope sc(s);
+        HIPCHK(hipStreamSynchronize(s->spec_stream));
     }
     for (int k = nshards() - 1; k >= 0; --k) {
         ShardScope sc(shard_ctx(k));
@@ -3487,7 +3713,7 @@ int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
     RC(need_init());
     // the caller may write through the pointer before the next pt_trace: a speculated next frame
     // summed from the image as it is now would then overwrite that write, so it is dropped here
-    RC(spec_cancel());
+    RC(spec_cancel_all());
     HIPCHK(hipStreamSynchronize(gp->stream));
     if (device_ptr) *device_ptr = gp->d_image;
     if (n_floats) *n_floats = (int64_t)gp->pixels_total * 3;
@@ -3496,7 +3722,7 @@ int32_t pt_get_image_device(void** device_ptr, int64_t* n_floats) {
 
 int32_t pt_set_image(const float* host_in, int64_t n_floats) {
     RC(need_init());
-    RC(spec_cancel());   // its image + plane was formed from the image being replaced
+    RC(spec_cancel_all());   // its image + plane was formed from the image being replaced
     if (!host_in || n_floats != (int64_t)gp->pixels_total * 3) return fail(PT_E_INVALID, "image size mismatch");
     for (int k = 0; k < nshards(); ++k) {   // each shard keeps accumulating into its own pixels of it
         ShardScope sc(shard_ctx(k));

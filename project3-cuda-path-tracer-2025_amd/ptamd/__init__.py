@@ -99,6 +99,7 @@ ABI_SYMBOLS = [
     "pt_debug_section_counters", "pt_texture_load",
     "pt_save_png", "pt_scene_load_ex", "pt_bvh_build", "pt_bvh_build_last_error", "pt_test_shade", "pt_test_compact", "pt_test_sort", "pt_test_rng", "pt_test_pbo", "pt_profile_frames", "pt_prepare_frames",
     "pt_device_alloc", "pt_device_free", "pt_device_read", "pt_set_trace_depth", "pt_set_speculation",
+    "pt_debug_spec_counts",
 ]
 # include/pt/pt_viewer.h (the headless interactive viewer)
 VIEWER_SYMBOLS = [
@@ -135,7 +136,7 @@ def _load():
         "pt_scene_load_ex": (i32, [ctypes.c_char_p, i32, i32, i32, i32, vp]),
         "pt_bvh_build": (i32, [vp, i32, vp, i32, vp, vp]),
         "pt_bvh_build_last_error": (ctypes.c_char_p, []),
-        "pt_set_trace_depth": (i32, [i32]), "pt_set_speculation": (i32, [i32]),
+        "pt_set_trace_depth": (i32, [i32]), "pt_set_speculation": (i32, [i32]), "pt_debug_spec_counts": (i32, [vp, vp]),
         "pt_device_alloc": (i32, [i64, vp]), "pt_device_free": (i32, [vp]), "pt_device_read": (i32, [vp, vp, i64]),
         "pt_viewer_create": (i32, [vp, vp, ctypes.c_char_p, ctypes.c_char_p, vp]), "pt_viewer_destroy": (None, [vp]),
         "pt_viewer_mouse_button": (i32, [vp, i32, i32, i32]),
@@ -338,6 +339,12 @@ class PathTracer:
         """Next-frame speculation of single-frame calls that copy the image out (default on)."""
         _check(lib.pt_set_speculation(int(bool(enabled))), "pt_set_speculation")
 
+    def spec_counts(self):
+        """(frames speculated, frames taken over) since init, over every shard."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _check(lib.pt_debug_spec_counts(ctypes.byref(a), ctypes.byref(b)), "pt_debug_spec_counts")
+        return a.value, b.value
+
     def trace_frames(self, first_iteration: int, count: int):
         _check(lib.pt_trace_frames(int(first_iteration), int(count)), "pt_trace_frames")
         self.iteration = first_iteration + count - 1
@@ -402,6 +409,9 @@ class PathTracer:
         out["tail_lanes_hist"] = [int(buf[len(self.SECTIONS) + 16 + i]) for i in range(16)]
         out["tail_by_sp"] = [int(buf[len(self.SECTIONS) + 32 + i]) for i in range(16)]
         out["tail_by_hit"] = [int(buf[len(self.SECTIONS) + 48 + i]) for i in range(4)]
+        # candidate-table scenes: superset sizes summed over live lanes, and the waves' maxima
+        out["n_sup"] = int(buf[len(self.SECTIONS) + 52])
+        out["n_sup_wmax"] = int(buf[len(self.SECTIONS) + 53])
         return out
 
     # ---- single-kernel entry points (tests) ----

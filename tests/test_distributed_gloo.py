@@ -127,3 +127,14 @@ def test_bench_refuses_world_size_mismatch():
     p = subprocess.run([sys.executable, os.path.join(os.path.dirname(PKG), "bench.py"), "--gpus", "1"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """RCCL ranks are one per GPU: a world larger than the visible devices is refused before any
+    GPU work (gloo rehearsals, PT_BENCH_BACKEND=gloo, may share a GPU)"""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", HIP_VISIBLE_DEVICES="")
+    env.pop("PT_BENCH_BACKEND", None)
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(PKG), "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "RCCL ranks" in p.stderr, p.stderr[-400:]

@@ -44,6 +44,12 @@ def _check_frame(tr, r, a, it, td):
     ("cornell", (64, 64), {}),
     ("cornell_glass_test", (64, 48), {"material_sort": 1}),
     ("cornell_obj_bnnuy", (64, 64), {}),
+    # several device contexts (shards sharing GPU 0 on the test box): every shard speculates its
+    # own pixels, the call for N + 1 takes each over and combines them (peer pull / RCCL group)
+    ("cornell", (64, 64), {"devices": [0, 0]}),
+    ("cornell_glass_test", (64, 48), {"material_sort": 1, "devices": [0, 0, 0], "combine": "rccl"}),
+    ("cornell_obj_bnnuy", (64, 64), {"devices": [0, 0, 0], "combine": "rccl"}),
+    ("cornell_obj_bnnuy", (64, 64), {"devices": [0, 0, 0, 0]}),
 ])
 def test_speculated_api_frames_bitexact(name, res, opts, oracle, ptamd, monkeypatch):
     monkeypatch.delenv("PT_SPECULATE", raising=False)
@@ -55,6 +61,8 @@ def test_speculated_api_frames_bitexact(name, res, opts, oracle, ptamd, monkeypa
     try:
         for it in (1, 2, 3, 4):                      # consecutive: frames 2..4 were speculated
             _check_frame(tr, r, a, it, td)
+        launched, adopted = tr.spec_counts()
+        assert adopted == 3 * len(opts.get("devices", [0])) and launched >= adopted, (launched, adopted)
         for it in (6, 7, 7, 8):                      # a skipped and a repeated iteration
             _check_frame(tr, r, a, it, td)
         tr.set_trace_depth(3)                        # depth change: the speculated frame is dropped
@@ -82,7 +90,8 @@ def test_speculated_api_frames_bitexact(name, res, opts, oracle, ptamd, monkeypa
         ptamd.lib.pt_init_data_container(None)
 
 
-def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_speculation_on_off_identical_with_pbo(devices, oracle, ptamd, monkeypatch):
     """the same call sequence with PT_SPECULATE=0 and with speculation: images and PBOs equal;
     a call without the host copy in the middle takes over the frame the previous one started"""
     a, b = _pair(oracle, ptamd, "cornell_glass_test", (48, 48))
@@ -92,7 +101,7 @@ def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
     try:
         for mode in ("0", "1"):
             monkeypatch.setenv("PT_SPECULATE", mode)
-            tr = ptamd.PathTracer(b)
+            tr = ptamd.PathTracer(b, **({} if devices is None else {"devices": devices}))
             imgs, pbos = [], []
             for it in (1, 2, 3, 5, 6, 7, 8):
                 tr.trace(it, pbo_device_ptr=pbo.value, copy_image=it != 6)
@@ -108,7 +117,8 @@ def test_speculation_on_off_identical_with_pbo(oracle, ptamd, monkeypatch):
         assert _eq(x, y)
 
 
-def test_camera_change_drops_the_speculated_frame(oracle, ptamd, monkeypatch):
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_camera_change_drops_the_speculated_frame(devices, oracle, ptamd, monkeypatch):
     """pt_set_camera with a different camera between frames: the frame traced after it uses the
     new camera (equal to a fresh tracer on the moved camera); setting the SAME camera keeps it.
     (Speculation starts only in calls that copy the image out, as main.cpp's do.)"""
@@ -117,7 +127,8 @@ def test_camera_change_drops_the_speculated_frame(oracle, ptamd, monkeypatch):
     b2 = ptamd.SceneFile(scene_path("cornell"), res=(48, 48))
     cam = b2.camera.copy()
     cam["position"][0][1] += 0.25                 # eye moved up
-    tr = ptamd.PathTracer(b)
+    dev = {} if devices is None else {"devices": devices}
+    tr = ptamd.PathTracer(b, **dev)
     tr.trace(1, copy_image=True)
     tr.trace(2, copy_image=True)
     assert ptamd.lib.pt_set_camera(b.camera.ctypes.data) == 0      # unchanged
@@ -128,7 +139,7 @@ def test_camera_change_drops_the_speculated_frame(oracle, ptamd, monkeypatch):
     tr.free()
     # reference: frames 1..3 on the old camera, then frame 4 on the moved one, no speculation
     monkeypatch.setenv("PT_SPECULATE", "0")
-    t2 = ptamd.PathTracer(b)
+    t2 = ptamd.PathTracer(b, **dev)
     for it in (1, 2, 3):
         t2.trace(it)
     assert _eq(t2.image(), base)

@@ -31,14 +31,17 @@ def passes(ptamd, sc, k, **opts):
     return round(1e3 * best / k, 4)
 
 
-def api(ptamd, sc, frames=40, **opts):
+def api(ptamd, sc, frames=40, copy=False, speculate=True, **opts):
+    """ms per pathtrace() call; copy: the image copied to host memory every call (main.cpp's call,
+    which is what starts the next-frame speculation; speculate=False turns it off)"""
     tr = ptamd.PathTracer(sc, **opts)
+    tr.set_speculation(speculate)
     for it in range(1, 6):
-        tr.trace(it)
+        tr.trace(it, copy_image=copy)
     tr.synchronize()
     t0 = time.perf_counter()
     for it in range(6, 6 + frames):
-        tr.trace(it)
+        tr.trace(it, copy_image=copy)
     tr.synchronize()
     dt = (time.perf_counter() - t0) / frames
     tr.free()
@@ -72,10 +75,15 @@ def main():
     out = {"scene": "cornell.json 800x800 depth 8", "frames_per_call": k, "unit": "ms per frame"}
     out["passes"] = {"1 context": passes(ptamd, sc, k)}
     out["api"] = {"1 context": api(ptamd, sc)}
+    # with the host copy (main.cpp's call): next-frame speculation on / off
+    out["api_copy"] = {"1 context": api(ptamd, sc, copy=True)}
+    out["api_copy_no_speculation"] = {"1 context": api(ptamd, sc, copy=True, speculate=False)}
     for n, comb in ((2, "peer"), (4, "peer"), (8, "peer"), (2, "rccl"), (8, "rccl")):
         key = f"{n} shards on device 0, {comb}"
         out["passes"][key] = passes(ptamd, sc, k, devices=[0] * n, combine=comb)
         out["api"][key] = api(ptamd, sc, devices=[0] * n, combine=comb)
+        out["api_copy"][key] = api(ptamd, sc, copy=True, devices=[0] * n, combine=comb)
+        out["api_copy_no_speculation"][key] = api(ptamd, sc, copy=True, speculate=False, devices=[0] * n, combine=comb)
     out["enqueue_us_per_shard"] = {}
     if os.environ.get("PT_MULTI_F1_DIRECT"):
         out["note"] = "PT_MULTI_F1_DIRECT=1: single-frame passes of shards launched directly (no graph)"

@@ -37,7 +37,10 @@ for s in "$@"; do
             [ -z "${AB_SKIP_CORNELL:-}" ] && AB_TAG=${tag}_cornell AB_ARGS="--steps 20 --warmup 5" step ab_${tag}_cornell 400 bash tools/ab_libs.sh
             AB_TAG=${tag}_bunny AB_ARGS="--steps 20 --warmup 5 --scene scenes/cornell_obj_bnnuy.json" step ab_${tag}_bunny 500 bash tools/ab_libs.sh
             AB_TAG=${tag}_khaslana AB_ARGS="--steps 10 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_${tag}_khaslana 600 bash tools/ab_libs.sh ;;
-        profiles) step profiles 1100 bash tools/r05_profiles.sh ;;
+        profiles) step profiles 1100 bash tools/r06_profiles.sh ;;
+        profstats) step profiles_stats 600 bash tools/r06_profiles.sh stats ;;
+        profpmc) step profiles_pmc 900 bash tools/r06_profiles.sh pmc ;;
+        profsec) step profiles_sec 600 bash tools/r06_profiles.sh sections ;;
         apicopy)
             step prof_api_copy 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/prof_api_copy -o run --output-format csv -- python tools/api_trace.py run copy
             python tools/api_trace.py overlap gpurun_out/prof_api_copy/run_kernel_trace.csv gpurun_out/prof_api_copy/run_memory_copy_trace.csv --out gpurun_out/api_copy_overlap.json ;;
@@ -58,6 +61,20 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        fusedtest) step pytest_fused 600 $PYT tests/test_bvh_tail.py tests/test_sort_next.py -m gpu -k "fused or sorted" ;;
+        fused5ab) L=$PWD/project3-cuda-path-tracer-2025_amd/build/ab
+            ARMS="- PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw5.so"
+            AB_ROUNDS=2 AB_TAG=fused5_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_fused5_bunny 600 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=fused5_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_fused5_cyrene 600 bash tools/ab_env.sh ;;
+        sortab) ARMS="- PT_SORT_NEXT=1 PT_SORT_NEXT=1,PT_BVH_TAIL_FUSED=1"
+            AB_TAG=sort_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 10 --warmup 2" step ab_sort_khaslana 900 bash tools/ab_env.sh
+            PT_SECTIONS_SKIP_CAMERA=1 step sec_khaslana_sort0 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana_sort0.json
+            PT_SECTIONS_SKIP_CAMERA=1 PT_SORT_NEXT=1 step sec_khaslana_sort1 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana_sort1.json ;;
+        fusedab) L=$PWD/project3-cuda-path-tracer-2025_amd/build/ab
+            ARMS="- PT_BVH_TAIL_FUSED=1 PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw5.so PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw7.so"
+            AB_TAG=fused_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_fused_bunny 900 bash tools/ab_env.sh
+            AB_TAG=fused_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 10 --warmup 2" step ab_fused_khaslana 900 bash tools/ab_env.sh
+            AB_TAG=fused_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_fused_cyrene 900 bash tools/ab_env.sh ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
