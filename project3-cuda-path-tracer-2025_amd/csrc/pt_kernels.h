@@ -83,7 +83,6 @@ struct SceneDev {
     const unsigned long long* grid;
     unsigned long long grid_all;   // every geom (rays outside the table's domain)
     float grid_lo[3], grid_inv[3]; // cell = floor((o - grid_lo) * grid_inv), GRID_G per axis
-    int sort_next;                 // k_bounce orders its survivors by their next superset's size (grid != null)
 };
 
 // The candidate table's resolution: GRID_G^3 origin cells x 6 faces x GRID_B^2 direction bins

@@ -314,59 +314,6 @@ PT_DEV void block_append(bool f0, int* ctr0, bool f1, int* ctr1, int& i0, int& i
     i1 = TWO ? s_b[1] + s_w[1][w] + mbcnt(m1) : 0;
 }
 
-// block_append for flag 0 with its survivors ordered by a key (0..15) within the block's output
-// chunk: (key, wave, lane) order, so that the next bounce's waves -- which take consecutive paths
-// -- hold paths of like key.  Same atomics as block_append (one per counter per block), no extra
-// barrier: each wave's lanes 0..15 count their key among the wave's flagged lanes from four
-// ballots, wave 0 scans the 64 (key, wave) counts.  `sk`: 70 ints of LDS that no thread reads
-// after the caller's last barrier.  Every thread of the block must call it.
-template <bool TWO>
-PT_DEV void block_append_keyed(bool f0, int key, int* ctr0, bool f1, int* ctr1, int& i0, int& i1, int* sk) {
-    int* s_k = sk;            // [wave][key] counts, then the (key, wave) exclusive offsets
-    int* s_w1 = sk + 64;      // flag 1 per wave
-    int* s_b = sk + 68;       // the two atomics' bases
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t m0 = __ballot(f0);
-    uint64_t bb[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) bb[b] = __ballot(f0 && ((key >> b) & 1));
-    const uint64_t m1 = TWO ? __ballot(f1) : 0ull;
-    auto peers = [&](int k) {
-        uint64_t m = m0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) m &= ((k >> b) & 1) ? bb[b] : ~bb[b];
-        return m;
-    };
-    if (lane < 16) s_k[w * 16 + lane] = __popcll(peers(lane));
-    if (TWO && lane == 0) s_w1[w] = __popcll(m1);
-    __syncthreads();
-    if (w == 0) {   // entry lane = key * 4 + wave, in that order
-        const int k = lane >> 2, ww = lane & 3;
-        const int v = s_k[ww * 16 + k];
-        int incl = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
-        const int tot = __shfl(incl, 63, 64);
-        s_k[ww * 16 + k] = incl - v;
-        if (lane == 0) s_b[0] = tot ? atomicAdd(ctr0, tot) : 0;
-    } else if (TWO && tid == 64) {
-        int tot = 0;
-#pragma unroll
-        for (int i = 0; i < BLOCK / 64; ++i) {
-            const int c = s_w1[i];
-            s_w1[i] = tot;
-            tot += c;
-        }
-        s_b[1] = tot ? atomicAdd(ctr1, tot) : 0;
-    }
-    __syncthreads();
-    i0 = f0 ? s_b[0] + s_k[w * 16 + key] + mbcnt(peers(key)) : 0;
-    i1 = TWO ? s_b[1] + s_w1[w] + mbcnt(m1) : 0;
-}
-
 template <bool FIRST, bool HAS_BVH, int VAR>
 __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathBuf out, FrameCtl* ctl,
                                                   float* __restrict__ image, int bounce, int seg_stride,
@@ -510,20 +457,7 @@ __global__ __launch_bounds__(BLOCK) void k_bounce(SceneDev sc, PathBuf in, PathB
     }
     // block-aggregated compaction (+ the traversal queue): one atomic per counter per block
     int si, qi;
-    // candidate-table scenes (SceneDev::sort_next): survivors ordered in the block's chunk by the
-    // size of their next pre-test superset, so that the next bounce's per-lane superset loop
-    // (cull_candidates_grid, which costs a wave its largest superset) meets like sizes in a wave.
-    // The exchange's ray rows are free here: their readers all precede block_intersect's last barrier.
-    // (mesh kernels only: the reference's candidate-table scenes are mesh scenes, and the
-    // primitive-only kernels keep their scalar registers)
-    constexpr bool KEYED = HAS_BVH && REDIST && (VAR & VAR_BLOCK_REDIST) && !MG;
-    if (KEYED && sc.sort_next && lds_geoms) {
-        const int key = surv ? min(15, __popcll(grid_superset(sc, p.o, p.d))) : 0;
-        block_append_keyed<SPLIT>(surv, key, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si,
-                                  qi, reinterpret_cast<int*>(reinterpret_cast<BlockLds*>(s_wave_isect - (tid >> 6))->ro[0]));
-    } else {
-        block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
-    }
+    block_append<SPLIT>(surv, &ctl->cnt[bounce + 1][seg][0], queued, &ctl->qcnt[bounce][seg][0], si, qi);
     if (surv) store_path(out, seg * seg_stride + si, p);
     qi += seg * q.stride;
     if (SPLIT && queued) queue_put(q, qi, p, qt, qw, qs);
@@ -788,111 +722,6 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
         }
     }
 }
-// k_bvh_tail_trav with the shading folded in (PT_BVH_TAIL_FUSED=1): a finished ray is not written
-// back for k_bvh_tail_shade but waits in its lane; whenever the wave would refill (or has nothing
-// left to traverse), its finished lanes are shaded together -- the queue entry's other words, the
-// hit, shade_path, the gather of a terminated path -- and the survivors appended to the output
-// segment with one atomic per wave.  Saves the final hit's write and read, the entry's re-read of
-// slot and hit, and k_bvh_tail_shade's launch; the shading runs at the refill's lane count.
-#ifndef TAIL_FUSED_WAVES
-#define TAIL_FUSED_WAVES 6
-#endif
-template <int VAR>
-__global__ __launch_bounds__(BLOCK, TAIL_FUSED_WAVES) void k_bvh_tail_fused(SceneDev sc, QueueBuf q, TailBuf t, PathBuf out,
-                                                                     FrameCtl* ctl, float* __restrict__ image,
-                                                                     int bounce, int refill, int seg_stride) {
-    extern __shared__ float4 s_dyn[];
-    int* s_stack = reinterpret_cast<int*>(s_dyn) + threadIdx.x;
-    const int seg = blockIdx.x & (NSEG - 1);
-    const int n = min(ctl->qcnt[bounce][seg][1], t.stride);
-    if (n == 0) return;
-    const int iter = ctl->iter;
-    const bool to_plane = ctl->batch > 1 || ctl->plane != 0;
-    const int lane = threadIdx.x & 63;
-    int next = 0;   // the segment's next untaken entry, as of this wave's last refill
-    constexpr bool CNT = (VAR & VAR_SECTION_TIMING) != 0;
-    int e = -1, qs = 0, n_nodes = 0, n_tris = 0, sp0 = 0;
-    bool hit0 = false;
-    TravState st;
-    st.cur = -1;
-    while (true) {
-        const bool fin = e >= 0 && st.cur < 0;              // traversed, not yet shaded
-        const uint64_t free_m = __ballot(e < 0 || fin);
-        const int n_free = __popcll(free_m);
-        const bool more = next < n;
-        if (n_free >= refill || n_free == 64) {   // (64: nothing is traversing)
-            if (__ballot(fin) != 0) {   // shade the finished lanes together
-                PathReg p;
-                p.rb = 0;
-                if (fin) {
-                    p.o = st.ro;
-                    p.d = st.rd;
-                    bvh_finish_path<VAR>(sc, q, qs, iter, p, st);
-                }
-                const bool surv = fin && p.rb > 0;
-                if (fin && !surv) gather_into_image(image, sc, to_plane, p);
-                const uint64_t m = __ballot(surv);
-                if (m != 0) {
-                    const int lead = __builtin_ctzll(m);
-                    int base = 0;
-                    if (lane == lead) base = atomicAdd(&ctl->cnt[bounce + 1][seg][0], __popcll(m));
-                    base = __builtin_amdgcn_readlane(base, lead);
-                    if (surv) store_path(out, seg * seg_stride + base + mbcnt(m), p);
-                }
-                if (fin) e = -1;
-            }
-            if (more) {
-                const uint64_t idle = __ballot(e < 0);
-                const int n_idle = __popcll(idle);
-                const int lead = __builtin_ctzll(idle);
-                int b0 = 0;
-                if (lane == lead) b0 = atomicAdd(&ctl->qcnt[bounce][seg][2], n_idle);
-                next = __builtin_amdgcn_readlane(b0, lead);
-                if (e < 0) {
-                    const int k = next + mbcnt(idle);
-                    if (k < n) {
-                        e = seg * t.stride + k;
-                        const int2 nd = t.node[e];
-                        qs = nd.x;
-                        const float4 a = q.A[qs], b = q.B[qs];
-                        trav_resume(st, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), t.hit[e], nd.y);
-                        for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK] = t.stack[(size_t)i * t.cap + e];
-                        n_nodes = n_tris = 0;
-                        if (CNT) {
-                            sp0 = st.sp;
-                            hit0 = st.btri != 0x7fffffff;
-                        }
-                    }
-                }
-                next += n_idle;
-            }
-        }
-        const bool trav = e >= 0 && st.cur >= 0;
-        const int lanes = __popcll(__ballot(trav));
-        if (lanes == 0) {
-            if (__ballot(e >= 0) == 0 && next >= n) break;   // nothing left to shade or take
-            continue;
-        }
-        if (trav) {
-            if (CNT) {
-                sec_add(SEC_N_BVH_WITERS, 1);
-                sec_add(SEC_TAIL_LANES_HIST + (lanes - 1) / 4, 1);
-            }
-            trav_step<CNT>(sc, st, s_stack, n_nodes, n_tris);
-            if (CNT && st.cur < 0) {
-                sec_add_lanes(SEC_N_NODES, n_nodes);
-                sec_add_lanes(SEC_N_TRIS, n_tris);
-                bvh_count_ray<CNT>(st, q.D[qs].x, n_nodes);
-                const int bk = sp0 < 4 ? sp0 : sp0 < 6 ? 4 : sp0 < 8 ? 5 : sp0 < 12 ? 6 : 7;
-                sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk, 1);
-                sec_add_lanes(SEC_TAIL_BY_SP + 2 * bk + 1, n_nodes);
-                sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 2 : 0), 1);
-                sec_add_lanes(SEC_TAIL_BY_HIT + (hit0 ? 3 : 1), n_nodes);
-            }
-        }
-    }
-}
-
 // ... and their shading, gather and compaction, as k_bvh_bounce's: block b takes the chunks
 // j = b / NSEG, + gridDim / NSEG, .. of BLOCK entries of segment s = b % NSEG, survivors to output
 // segment s (a grid for the usual counts, not for the capacity: empty blocks cost dispatch time)
@@ -1318,13 +1147,11 @@ struct Tuning {
     int64_t auto_paths = 0;                         // PT_AUTO_PATHS: auto pass size in paths (0: AUTO_BATCH_PATHS)
     bool f1_graph = false;                          // PT_F1_GRAPH=1: single-frame passes through a graph
     bool multi_f1_direct = false;                   // PT_MULTI_F1_DIRECT=1: shards' single frames launched directly
-    int bvh_tail_lanes = 32;                        // PT_BVH_TAIL_LANES (0..56; 0: no hand-over)
+    int bvh_tail_lanes = -1;                        // PT_BVH_TAIL_LANES (0..56; 0: no hand-over; -1: by tree size)
     int bvh_tail_chunks = 0;                        // PT_BVH_TAIL_CHUNKS: capped hand-over buffers (tests)
     int tail_refill = 16;                           // PT_BVH_TAIL_REFILL (1..64 idle lanes)
     int tail_trav_blocks = 224;                     // PT_BVH_TAIL_TRAV_BLOCKS per segment
     int tail_shade_blocks = 512;                    // PT_BVH_TAIL_SHADE_BLOCKS per segment (0: one per chunk)
-    bool sort_next = false;                         // PT_SORT_NEXT=1: SceneDev::sort_next (candidate-table scenes)
-    bool tail_fused = false;                        // PT_BVH_TAIL_FUSED=1: k_bvh_tail_fused (shading in the refilling waves)
     bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
     bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
@@ -1346,13 +1173,11 @@ Tuning read_tuning() {
     t.auto_paths = num("PT_AUTO_PATHS", 0);
     t.f1_graph = num("PT_F1_GRAPH", 0) != 0;
     t.multi_f1_direct = num("PT_MULTI_F1_DIRECT", 0) != 0;
-    t.bvh_tail_lanes = (int)std::min(56L, std::max(0L, num("PT_BVH_TAIL_LANES", 32)));
+    t.bvh_tail_lanes = (int)std::min(56L, std::max(-1L, num("PT_BVH_TAIL_LANES", -1)));
     t.bvh_tail_chunks = (int)std::max(0L, num("PT_BVH_TAIL_CHUNKS", 0));
     t.tail_refill = (int)std::max(1L, std::min(64L, num("PT_BVH_TAIL_REFILL", 16)));
     t.tail_trav_blocks = (int)std::max(1L, num("PT_BVH_TAIL_TRAV_BLOCKS", 224));
     t.tail_shade_blocks = (int)std::max(0L, num("PT_BVH_TAIL_SHADE_BLOCKS", 512));
-    t.tail_fused = num("PT_BVH_TAIL_FUSED", 0) != 0;
-    t.sort_next = num("PT_SORT_NEXT", 0) != 0;
     t.combine_force_staged = num("PT_COMBINE_FORCE_STAGED", 0) != 0;
     const char* tree = getenv("PT_BVH_TREE");
     t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
@@ -1559,10 +1384,7 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
         if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
         launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail,
                gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
-        if (gp->tail_lanes > 0 && gp->tune.tail_fused) {   // refilling waves that shade what they finish
-            launch(400 + b, k_bvh_tail_fused<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
-                   gp->queue, gp->tail, out, gp->d_ctl, gp->d_image, b, gp->tail_refill, gp->seg_stride);
-        } else if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
+        if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
             launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
                    gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
             const int per_seg = gp->tail_shade_blocks > 0 ? std::min(gp->tail_shade_blocks, nblocks(gp->tail.stride))
@@ -2250,8 +2072,14 @@ int q_stride_for(int frames) {
     return ((nb + NSEG - 1) / NSEG) * BLOCK;
 }
 // k_bvh_bounce hands a wave's traversals to k_bvh_tail_trav once no more than this many of its lanes
-// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56)
-int bvh_tail_lanes() { return gp->tune.bvh_tail_lanes; }
+// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56).  By default 40, and 48 for trees
+// of 65,536 refs or more (stack entries with refs wider than 16 bits): deeper traversals diverge
+// more, so handing over earlier pays (A/B, profiles/r06_ab_tail_lanes.json: bunny / khaslana best
+// at 40, within 0.5 % of 32; the 262k / 1.0M-triangle stand-ins best at 48, 2-3 % below 32)
+int bvh_tail_lanes() {
+    if (gp->tune.bvh_tail_lanes >= 0) return gp->tune.bvh_tail_lanes;
+    return 32 - gp->sc.ref_shift > 16 ? 48 : 40;
+}
 // entries per tail segment: what k_bvh_bounce can hand over, `lanes` per wave of its blocks of one
 // segment.  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane that finds its segment
 // full then finishes its ray itself (tail_put).  A cap measured slower at every size tried:
@@ -3472,7 +3300,6 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.cull_c0 = (float)(64.0 * std::ldexp(1.0, -24) / 1e-5 * 1.01 * (1.0 + 1e-5));
     sc.cull_E = (float)(cull_extent * (1.0 + 1e-5));
     sc.grid = gp->d_grid;
-    sc.sort_next = gp->d_grid && gp->tune.sort_next ? 1 : 0;
     sc.grid_all = s->num_geoms >= 64 ? ~0ull : ((1ull << s->num_geoms) - 1);
     for (int a = 0; a < 3; ++a) {
         sc.grid_lo[a] = grid_lo[a];

@@ -54,35 +54,3 @@ def test_handed_over_traversals_bitexact(name, res, depth, lanes, chunks, refill
     finally:
         tr.free()
 
-
-@pytest.mark.parametrize("lanes,chunks,refill", [(32, 0, 16), (56, 0, 1), (24, 0, 64), (8, 1, 64)])
-@pytest.mark.parametrize("name,res,depth", [("cornell_obj_bnnuy", (96, 96), None),
-                                            ("cornell_obj_khaslana", (64, 64), 12),
-                                            ("cornell_obj_cyrene", (48, 48), None)])
-def test_fused_tail_shading_bitexact(name, res, depth, lanes, chunks, refill, oracle, ptamd, monkeypatch):
-    """PT_BVH_TAIL_FUSED=1: k_bvh_tail_fused shades the rays it finishes in the refilling waves
-    (no k_bvh_tail_shade); same images and live counts as the oracle."""
-    monkeypatch.setenv("PT_BVH_TAIL_FUSED", "1")
-    monkeypatch.setenv("PT_BVH_TAIL_REFILL", str(refill))
-    monkeypatch.setenv("PT_BVH_TAIL_LANES", str(lanes))
-    monkeypatch.setenv("PT_BVH_TAIL_CHUNKS", str(chunks))
-    a = oracle.load_scene(scene_path(name), res=res, depth=depth)
-    b = ptamd.SceneFile(scene_path(name), res=res, depth=depth)
-    r = oracle.Renderer(a, oracle.options(**BIT))
-    tr = ptamd.PathTracer(b)
-    try:
-        segs = 0
-        for it in range(1, 5):
-            segs += int(np.maximum(r.trace(it), 0).sum())
-        tr.trace_frames(1, 4)
-        st = tr.stats()
-        assert sum(st["handed_total"]) > 0 or lanes == 0
-        assert _eq(tr.image(), r.image), (name, lanes, chunks, refill)
-        assert st["segments_total"] == segs
-        for it in (5, 6):
-            live = r.trace(it)
-            tr.trace(it, copy_image=True)
-            assert tr.stats()["live"][:a.trace_depth] == [int(x) if x >= 0 else 0 for x in live][:a.trace_depth]
-        assert _eq(tr.image(), r.image), (name, lanes, chunks, refill)
-    finally:
-        tr.free()

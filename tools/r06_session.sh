@@ -61,20 +61,13 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
-        fusedtest) step pytest_fused 600 $PYT tests/test_bvh_tail.py tests/test_sort_next.py -m gpu -k "fused or sorted" ;;
-        fused5ab) L=$PWD/project3-cuda-path-tracer-2025_amd/build/ab
-            ARMS="- PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw5.so"
-            AB_ROUNDS=2 AB_TAG=fused5_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_fused5_bunny 600 bash tools/ab_env.sh
-            AB_ROUNDS=2 AB_TAG=fused5_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_fused5_cyrene 600 bash tools/ab_env.sh ;;
-        sortab) ARMS="- PT_SORT_NEXT=1 PT_SORT_NEXT=1,PT_BVH_TAIL_FUSED=1"
-            AB_TAG=sort_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 10 --warmup 2" step ab_sort_khaslana 900 bash tools/ab_env.sh
-            PT_SECTIONS_SKIP_CAMERA=1 step sec_khaslana_sort0 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana_sort0.json
-            PT_SECTIONS_SKIP_CAMERA=1 PT_SORT_NEXT=1 step sec_khaslana_sort1 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana_sort1.json ;;
-        fusedab) L=$PWD/project3-cuda-path-tracer-2025_amd/build/ab
-            ARMS="- PT_BVH_TAIL_FUSED=1 PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw5.so PT_BVH_TAIL_FUSED=1,PTAMD_LIB=$L/fw7.so"
-            AB_TAG=fused_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_fused_bunny 900 bash tools/ab_env.sh
-            AB_TAG=fused_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 10 --warmup 2" step ab_fused_khaslana 900 bash tools/ab_env.sh
-            AB_TAG=fused_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_fused_cyrene 900 bash tools/ab_env.sh ;;
+        lanesall) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=32 PT_BVH_TAIL_LANES=40 PT_BVH_TAIL_LANES=48 PT_BVH_TAIL_LANES=56}"
+            AB_ROUNDS=2 AB_TAG=lanes_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lanes_bunny 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=lanes_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 32 --warmup 2" step ab_lanes_khaslana 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=lanes_cyrene2 AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_lanes_cyrene2 900 bash tools/ab_env.sh ;;
+        lanesbig) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=0 PT_BVH_TAIL_LANES=16 PT_BVH_TAIL_LANES=32 PT_BVH_TAIL_LANES=48}"
+            AB_ROUNDS=2 AB_TAG=lanes_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_lanes_cyrene 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=lanes_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_lanes_phainon 900 bash tools/ab_env.sh ;;
         empty) step empty_probe 120 project3-cuda-path-tracer-2025_amd/build/empty_block_probe ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
