@@ -1155,6 +1155,8 @@ struct Tuning {
     bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
     bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
+    int bvh_bfs_levels = 1 << 30;                   // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
+                                                    // this many levels, each subtree below in preorder
     int grid = -1;                                  // PT_GRID: 0 no candidate table, 1 also for small scenes
     bool speculate = true;                          // PT_SPECULATE=0: initial state of pt_set_speculation
 };
@@ -1182,6 +1184,7 @@ Tuning read_tuning() {
     const char* tree = getenv("PT_BVH_TREE");
     t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
     t.bvh_tree_info = getenv("PT_BVH_TREE_INFO") != nullptr;
+    t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 1 << 30));
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
     return t;
@@ -1259,6 +1262,8 @@ struct State {
     float* d_spec_sum[2] = {nullptr, nullptr};   // image + plane, formed at its end (alternating)
     int spec_sum_idx = 0;                 // the buffer the pending speculative frame writes
     hipStream_t copy_stream = nullptr;    // the host copy of a taken-over frame's image
+    hipStream_t band_stream = nullptr;    // several devices: the host copy of this shard's row bands
+    hipEvent_t band_ready = nullptr;      // ... what it follows (the shard's frame)
     hipGraph_t spec_graph = nullptr;      // its pass, captured once (released with the pass graphs)
     hipGraphExec_t spec_exec = nullptr;
     int spec_iter = 0;                    // iteration of the queued speculative frame (0: none)
@@ -1726,6 +1731,115 @@ struct SpecLauncher {
     ~SpecLauncher() { join(); }   // a process that exits without pt_free: an idle thread, stopped
 };
 SpecLauncher g_spec_launcher;
+
+// ---- several devices: the host copy split over the shards' own links --------------------------
+// main.cpp's pathtrace() copies the whole image to pageable host memory every call
+// (pathtrace.cu:783).  From one device that copy crosses one PCIe link (~0.14 ms at 800^2, longer
+// than the frame).  With several devices each shard copies its own row bands from its own device,
+// so the devices' links run side by side.  A copy into pageable memory holds the thread that
+// issues it until it is done, so shard k's copy is issued by helper thread k (shard 0's by the
+// caller).  The helpers keep INTEGRATION.md's threading rules: a helper gets copied values only
+// (its shard's device and band stream, the event the caller recorded after the shard's frame, the
+// two image bases and the band geometry), calls nothing but those HIP copies, and the call waits
+// for every helper before it returns.
+struct BandCopy {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr;
+    const char* src = nullptr;     // a full-size image on the shard's device (same layout as dst)
+    char* dst = nullptr;           // the caller's host image
+    size_t first = 0, pitch = 0, width = 0, height = 0;   // `height` bands of `width` bytes, `pitch` apart
+    size_t tail_off = 0, tail_bytes = 0;                 // a shorter last band (0 bytes: none)
+    hipError_t run() const {
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, ready, 0);
+        if (e == hipSuccess && height > 0)
+            e = hipMemcpy2DAsync(dst + first, pitch, src + first, pitch, width, height, hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess && tail_bytes > 0)
+            e = hipMemcpyAsync(dst + tail_off, src + tail_off, tail_bytes, hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        return e;
+    }
+};
+struct CopyHelper {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool task = false, busy = false, stop = false;
+    hipError_t err = hipSuccess;
+    BandCopy job;
+    void run_loop() {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return task || stop; });
+            if (stop) return;
+            task = false;
+            const BandCopy j = job;
+            lk.unlock();
+            const hipError_t e = j.run();
+            lk.lock();
+            err = e;
+            busy = false;
+            cv.notify_all();
+        }
+    }
+    void post(const BandCopy& j) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!th.joinable()) th = std::thread([this] { run_loop(); });
+        job = j;
+        task = busy = true;
+        cv.notify_all();
+    }
+    hipError_t wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !busy; });
+        const hipError_t e = err;
+        err = hipSuccess;
+        return e;
+    }
+    void join() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        if (th.joinable()) th.join();
+        stop = false;
+    }
+    ~CopyHelper() { join(); }
+};
+CopyHelper g_copy_helpers[PT_MAX_DEVICES];
+
+// the current shard's row bands of `src` (a full-size image on its device: its own pixels are
+// final) into the host image, after the work queued so far on `after`
+int band_prepare(BandCopy& b, float* host, const float* src, hipStream_t after) {
+    if (!gp->band_stream) {
+        HIPCHK(hipStreamCreateWithFlags(&gp->band_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&gp->band_ready, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(gp->band_ready, after));
+    const ShardDev& sd = gp->sc.shard;
+    const size_t W = (size_t)gp->width, H = (size_t)gp->height, R = (size_t)std::max(1, sd.rows);
+    const size_t N = (size_t)std::max(1, sd.count), k = (size_t)sd.rank, row = 3 * sizeof(float) * W;
+    const size_t nb = (H + R - 1) / R;                   // bands of the image; shard k has k, k + N, ..
+    size_t mine = k < nb ? (nb - 1 - k) / N + 1 : 0;
+    b = BandCopy();
+    b.device = gp->device;
+    b.stream = gp->band_stream;
+    b.ready = gp->band_ready;
+    b.src = reinterpret_cast<const char*>(src);
+    b.dst = reinterpret_cast<char*>(host);
+    b.width = R * row;
+    b.pitch = N * R * row;
+    b.first = k * R * row;
+    if (mine > 0 && (nb - 1) % N == k && H % R != 0) {   // the image's last band is shorter and ours
+        --mine;
+        b.tail_off = (nb - 1) * R * row;
+        b.tail_bytes = (H - (nb - 1) * R) * row;
+    }
+    b.height = mine;
+    return PT_OK;
+}
 int spec_worker_idle() {
     HIPCHK(g_spec_launcher.idle());
     return PT_OK;
@@ -2185,6 +2299,10 @@ int ensure_test_paths(int64_t n) {
 
 void free_all() {
     spec_release();
+    if (gp->band_stream) (void)hipStreamSynchronize(gp->band_stream), (void)hipStreamDestroy(gp->band_stream);
+    if (gp->band_ready) (void)hipEventDestroy(gp->band_ready);
+    gp->band_stream = nullptr;
+    gp->band_ready = nullptr;
     release_graph();
     free_pass_buffers();
     void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
@@ -2647,6 +2765,7 @@ int32_t pt_free(void) {
         }
     }
     M = Multi();
+    for (CopyHelper& h : g_copy_helpers) h.join();
     free_all();   // also resets g_primary's sizes (alloc_frames, capacity, ...) after a failed init
     return PT_OK;
 }
@@ -3070,7 +3189,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         lhi[3 * k] = nd.hi.x; lhi[3 * k + 1] = nd.hi.y; lhi[3 * k + 2] = nd.hi.z;
                         ls[k] = node_aux[leaf_nodes[k]].y;
                     }
-                    sah = pth::build_sah_tree(llo, lhi, ls, tt, th) && th + 1 <= MAXSTACK &&
+                    sah = pth::build_sah_tree(llo, lhi, ls, tt, th, gp->tune.bvh_bfs_levels) && th + 1 <= MAXSTACK &&
                           (int64_t)tt.size() + L < (1 << 24);
                     if (sah) {   // the union of the leaves is the reference root box, bit for bit
                         const pth::TravChild& a = tt[0].c[0];
@@ -3429,14 +3548,19 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     const bool single = M.n <= 1;
     bool adopted = false;
     const int sum_idx = gp->spec_sum_idx;   // the taken-over frame's image, before the next launch flips it
+    BandCopy bands[PT_MAX_DEVICES];
     for (int k = 0; k < nshards(); ++k) {
         ShardScope sc(shard_ctx(k));
         if (spec && gp->spec_iter == iteration) {
             adopted = true;
+            const float* sum = gp->d_spec_sum[gp->spec_sum_idx];
             RC(spec_adopt(host_image != nullptr && single));   // traced already, during the previous call's copy
+            // several devices: this shard's bands of the finished sum (the speculative stream has it)
+            if (!single && host_image) RC(band_prepare(bands[k], host_image, sum, gp->spec_stream));
         } else {
             RC(spec_cancel());
             RC(run_frame(iteration));
+            if (!single && host_image) RC(band_prepare(bands[k], host_image, gp->d_image, gp->stream));
         }
         if (g_primary.traced_depth) RC(frame_depth_enqueue());   // read after the one sync below
     }
@@ -3449,7 +3573,17 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     // the next frame, on the second stream, while this one's image is copied out (queued before
     // the copy: a copy into pageable memory may hold the host until it is done)
     if (spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
-    if (host_image) {
+    if (host_image && !single) {
+        // every shard's row bands from its own device, side by side (shard 0's on this thread)
+        for (int k = 1; k < nshards(); ++k) g_copy_helpers[k].post(bands[k]);
+        hipError_t e = bands[0].run();
+        for (int k = 1; k < nshards(); ++k) {
+            const hipError_t ek = g_copy_helpers[k].wait();
+            if (e == hipSuccess) e = ek;
+        }
+        HIPCHK(hipSetDevice(g_primary.device));
+        HIPCHK(e);
+    } else if (host_image) {
         // the caller's pageable memory, as cudaMemcpy(state.image) (pathtrace.cu:783).  It is not
         // page-locked: a registration would outlive a caller that frees the buffer and gets a new
         // one at the same address, and on MI355X the pageable copy runs at the pinned rate anyway

@@ -40,7 +40,7 @@ struct Tmp {
 }  // namespace
 
 bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>& leaf_hi,
-                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height) {
+                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height, int bfs_levels) {
     const int n = (int)leaf_s.size();
     out.clear();
     height = 0;
@@ -155,15 +155,38 @@ bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>&
         }
         T[i].s = std::max(s0, s1);
     }
-    // breadth-first numbering (the top levels share cache lines)
-    std::vector<int> order{0}, bfs(T.size(), -1);
+    // numbering: breadth-first over the top bfs_levels levels (they share a few cache lines), then
+    // every subtree below them in preorder -- T's own order (a parent is created before its
+    // children, a left subtree before its right one), so a subtree is one contiguous range of T
+    std::vector<int> order{0}, bfs(T.size(), -1), depth(T.size(), 0), roots;
     bfs[0] = 0;
-    for (size_t h = 0; h < order.size(); ++h)
-        for (int k : T[order[h]].kid)
+    for (size_t h = 0; h < order.size(); ++h) {
+        const int n = order[h];
+        if (depth[n] >= bfs_levels) {   // a subtree root: numbered below
+            roots.push_back(n);
+            continue;
+        }
+        for (int k : T[n].kid)
             if (k >= 0) {
-                bfs[k] = (int)order.size();
+                depth[k] = depth[n] + 1;
                 order.push_back(k);
             }
+    }
+    if (!roots.empty()) {
+        order.erase(std::remove_if(order.begin(), order.end(), [&](int n) { return depth[n] >= bfs_levels; }),
+                    order.end());
+        for (int r : roots) {   // preorder of r's subtree: T[r .. r + size)
+            std::vector<int> st{r};
+            while (!st.empty()) {
+                const int n = st.back();
+                st.pop_back();
+                order.push_back(n);
+                if (T[n].kid[1] >= 0) st.push_back(T[n].kid[1]);
+                if (T[n].kid[0] >= 0) st.push_back(T[n].kid[0]);
+            }
+        }
+    }
+    for (size_t h = 0; h < order.size(); ++h) bfs[order[h]] = (int)h;
     out.resize(T.size());
     for (size_t h = 0; h < order.size(); ++h) {
         const Tmp& t = T[order[h]];

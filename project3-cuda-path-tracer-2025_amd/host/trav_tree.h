@@ -26,10 +26,14 @@ struct TravInner {
 };
 
 // Binned-SAH tree over `n` leaves (boxes lo/hi as 3 floats each, cull sizes s).  Inner nodes are
-// numbered breadth-first, the root is inner node 0 (n >= 2).  `height`: levels of inner nodes plus
-// the leaf level.  Returns false for n < 2 or for a box with a NaN / infinite coordinate (the
-// containment argument needs ordered, finite bounds): the caller keeps the reference hierarchy.
+// numbered breadth-first over the top `bfs_levels` levels, then each subtree below them in
+// depth-first preorder (so a subtree's nodes share cache lines; a large value: breadth-first
+// throughout, 0: preorder throughout); the root is inner node 0 (n >= 2).  `height`: levels of
+// inner nodes plus the leaf level.  Returns false for n < 2 or for a box with a NaN / infinite
+// coordinate (the containment argument needs ordered, finite bounds): the caller keeps the
+// reference hierarchy.
 bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>& leaf_hi,
-                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height);
+                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height,
+                    int bfs_levels = 1 << 30);
 
 }  // namespace pth

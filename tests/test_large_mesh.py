@@ -153,3 +153,23 @@ def test_large_mesh_intersections_match_reference(name, variant, ptamd):
     tr.free()
     assert int((got["t"] > 0).sum()) == ref["hits"]
     assert R.digest(R.pack(got, R.P_ISECT)) == ref["isect_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levels", [0, 8])
+def test_pair_numbering_does_not_change_results(levels, oracle, ptamd, monkeypatch):
+    """PT_BVH_BFS_LEVELS: the SAH pairs numbered breadth-first over the top levels and in preorder
+    below (0: preorder throughout) -- only where the records live changes, not what is visited."""
+    monkeypatch.setenv("PT_BVH_BFS_LEVELS", str(levels))
+    name, res = LARGE[0]
+    a = oracle.load_scene(scene_path(name), res=res)
+    b = ptamd.SceneFile(scene_path(name), res=res)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr = ptamd.PathTracer(b)
+    try:
+        for it in range(1, 4):
+            r.trace(it)
+        tr.trace_frames(1, 3)
+        assert _eq(tr.image(), r.image), levels
+    finally:
+        tr.free()

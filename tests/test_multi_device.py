@@ -83,6 +83,11 @@ MULTI_CASES = [
     ("cornell_obj_bnnuy", (64, 64), [0, 0], "rccl", {}),
     ("cornell_obj_khaslana", (48, 48), [0, 0, 0], "peer", {}),
     ("cornell", (64, 64), [0, 0, 0], "peer", {"pipeline": 1}),
+    # host copy split over the shards' row bands: a shorter last band owned by a middle shard
+    # (61 rows = 7 bands of 8 + one of 5, band 7 -> shard 1), more shards than some get bands of
+    ("cornell", (64, 61), [0, 0, 0], "peer", {}),
+    ("cornell_glass_test", (40, 37), [0, 0, 0, 0, 0], "rccl", {"shard_rows": 2}),
+    ("cornell", (48, 20), [0, 0, 0], "peer", {"shard_rows": 8, "pipeline": 1}),
 ]
 
 

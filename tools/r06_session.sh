@@ -48,6 +48,7 @@ for s in "$@"; do
         hist) step sec_bunny 300 python -u tools/section_times.py --scene cornell_obj_bnnuy --variant 190 --frames 16 --out gpurun_out/sec_bunny.json
             step sec_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana.json ;;
         large) step pytest_large 600 $PYT tests/test_large_mesh.py -m gpu ;;
+        multitest) step pytest_multi 600 $PYT tests/test_multi_device.py tests/test_speculation.py tests/test_dropin.py -m gpu ;;
         benchlarge) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step bench_cyrene 300 $B --steps 24 --warmup 2 --scene scenes/cornell_obj_cyrene.json
             step bench_cyrene_nodes 300 $B --steps 8 --warmup 1 --scene scenes/cornell_obj_cyrene.json --variant 250
@@ -61,6 +62,10 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        orderab) ARMS="${ORDER_ARMS:-- PT_BVH_BFS_LEVELS=0 PT_BVH_BFS_LEVELS=8 PT_BVH_BFS_LEVELS=12}"
+            AB_ROUNDS=2 AB_TAG=order_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_order_cyrene 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=order_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_order_phainon 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=order_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_order_bunny 900 bash tools/ab_env.sh ;;
         lanesall) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=32 PT_BVH_TAIL_LANES=40 PT_BVH_TAIL_LANES=48 PT_BVH_TAIL_LANES=56}"
             AB_ROUNDS=2 AB_TAG=lanes_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_lanes_bunny 900 bash tools/ab_env.sh
             AB_ROUNDS=2 AB_TAG=lanes_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 32 --warmup 2" step ab_lanes_khaslana 900 bash tools/ab_env.sh
