@@ -1155,8 +1155,10 @@ struct Tuning {
     bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
     bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
-    int bvh_bfs_levels = 1 << 30;                   // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
+    int bvh_bfs_levels = 12;                        // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
                                                     // this many levels, each subtree below in preorder
+                                                    // (A/B: 262k -1.0 %, 1.0M -1.4 %, bunny +-0 vs all
+                                                    // breadth-first; profiles/r06_ab_pair_numbering.json)
     int grid = -1;                                  // PT_GRID: 0 no candidate table, 1 also for small scenes
     bool speculate = true;                          // PT_SPECULATE=0: initial state of pt_set_speculation
 };
@@ -1184,7 +1186,7 @@ Tuning read_tuning() {
     const char* tree = getenv("PT_BVH_TREE");
     t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
     t.bvh_tree_info = getenv("PT_BVH_TREE_INFO") != nullptr;
-    t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 1 << 30));
+    t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 12));
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
     return t;

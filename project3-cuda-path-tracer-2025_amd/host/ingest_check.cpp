@@ -59,9 +59,37 @@ static int check_scene(const char* path) {
     std::vector<pth::TravInner> tree;
     int height = 0;
     const bool sah = pth::build_sah_tree(lo, hi, s, tree, height);
-    std::printf("scene rc=0 geoms=%d materials=%d triangles=%d nodes=%d depth=%d textures=%d bad_tex=%d sah=%d\n",
+    // the same tree under every numbering (breadth-first top levels, preorder below): walk both
+    // from the root and compare every child's box, cull size and leaf id
+    int orders_equal = sah ? 1 : -1;
+    for (int levels : {0, 1, 4, 8}) {
+        if (!sah || s.size() > 20000) break;   // (the 262k / 1.0M stand-ins: too slow under ASan)
+        std::vector<pth::TravInner> t2;
+        int h2 = 0;
+        if (!pth::build_sah_tree(lo, hi, s, t2, h2, levels) || h2 != height || t2.size() != tree.size()) {
+            orders_equal = 0;
+            break;
+        }
+        std::vector<std::pair<int, int>> st{{0, 0}};
+        size_t seen = 0;
+        while (!st.empty() && orders_equal) {
+            const auto [a, b] = st.back();
+            st.pop_back();
+            ++seen;
+            for (int c = 0; c < 2; ++c) {
+                const pth::TravChild &x = tree[a].c[c], &y = t2[b].c[c];
+                bool same = x.leaf == y.leaf && x.s == y.s && (!x.leaf || x.ref == y.ref);
+                for (int k = 0; k < 3; ++k) same = same && x.lo[k] == y.lo[k] && x.hi[k] == y.hi[k];
+                if (!same) orders_equal = 0;
+                else if (!x.leaf) st.push_back({x.ref, y.ref});
+            }
+        }
+        if (seen != tree.size()) orders_equal = 0;
+    }
+    std::printf("scene rc=0 geoms=%d materials=%d triangles=%d nodes=%d depth=%d textures=%d bad_tex=%d sah=%d "
+                "sah_orders_equal=%d\n",
                 v.num_geoms, v.num_materials, v.num_triangles, v.num_bvh_nodes, depth, v.num_textures, bad_tex,
-                sah ? height : -1);
+                sah ? height : -1, orders_equal);
     pt_scene_free(f);
     return 0;
 }

@@ -77,6 +77,9 @@ def test_every_repository_scene_and_texture(driver):
     for n, r in res.items():   # the refusals are the reference's: absent OBJs, sphere.json's APERTURE
         if r.startswith("scene rc=-1"):
             assert "Failed to load" in r or "APERTURE" in r, (n, r)
+    # the SAH traversal tree is the same tree under every pair numbering (PT_BVH_BFS_LEVELS)
+    for n in ("cornell_obj_bnnuy.json", "cornell_obj_khaslana.json"):
+        assert "sah_orders_equal=1" in res[n], (n, res[n])
     pngs = sorted(glob.glob(os.path.join(REPO, "scenes", "textures", "*.png")) +
                   glob.glob(os.path.join(GOLDEN, "*.png")))
     if pngs:
