@@ -152,21 +152,28 @@ def inproc_main(args):
     it += args.steps * per_step
     st = tr.stats()
     assert st["frames_total"] == args.steps * per_step
-    # the API call (one frame per pathtrace(), image copied to host), as main.cpp:463 makes it
-    ts = []
-    for k in range(25):
-        t1 = time.perf_counter()
-        tr.trace(it + k, copy_image=True)
-        if k >= 5:
-            ts.append(1e3 * (time.perf_counter() - t1))
-    ts.sort()
+    # the API call (one frame per pathtrace(), image copied to host), as main.cpp:463 makes it: each
+    # shard speculates its next frame and copies its own row bands over its own link; then the same
+    # calls with the speculation off
+    def api_calls(first):
+        ts = []
+        for k in range(25):
+            t1 = time.perf_counter()
+            tr.trace(first + k, copy_image=True)
+            if k >= 5:
+                ts.append(1e3 * (time.perf_counter() - t1))
+        ts.sort()
+        return round(ts[len(ts) // 2], 4)
+    api_ms = api_calls(it)
+    tr.set_speculation(False)
+    api_ms_nospec = api_calls(it + 25)
     tr.free()
     out = {"metric": "Mpaths/s (rays x bounces / s), 800x800 cornell depth 8", "mode": "inproc",
            "value": round(st["segments_total"] / el / 1e6, 2), "unit": "Mpaths/s", "n_gpus": n,
            "devices": devices, "combine": args.combine, "steps": args.steps, "warmup": args.warmup,
            "frames_per_step": per_step, "ms_per_step": round(1e3 * el / args.steps, 4),
            "ms_per_frame": round(1e3 * el / (args.steps * per_step), 4),
-           "api_ms_per_frame": round(ts[len(ts) // 2], 4),
+           "api_ms_per_frame": api_ms, "api_ms_per_frame_no_speculation": api_ms_nospec,
            "parallelism": f"one process, pt_options.num_devices={n}: interleaved 8-row bands per device, "
                           f"one combine into device 0 per call ({args.combine})"}
     print(json.dumps(out), flush=True)

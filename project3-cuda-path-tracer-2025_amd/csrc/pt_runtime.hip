@@ -1161,6 +1161,9 @@ struct Tuning {
                                                     // breadth-first; profiles/r06_ab_pair_numbering.json)
     int grid = -1;                                  // PT_GRID: 0 no candidate table, 1 also for small scenes
     bool speculate = true;                          // PT_SPECULATE=0: initial state of pt_set_speculation
+    int band_copy = -1;                             // PT_BAND_COPY: several devices' host copy split over the
+                                                    // shards (1), one copy from the first device (0), or
+                                                    // split only when every shard has a device of its own (-1)
 };
 Tuning read_tuning() {
     auto num = [](const char* name, long dflt) {
@@ -1189,6 +1192,7 @@ Tuning read_tuning() {
     t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 12));
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
+    t.band_copy = (int)std::max(-1L, std::min(1L, num("PT_BAND_COPY", -1)));
     return t;
 }
 
@@ -2457,6 +2461,7 @@ struct Multi {
     ncclComm_t comm[PT_MAX_DEVICES] = {};
     hipStream_t cstream[PT_MAX_DEVICES] = {};
     hipEvent_t cdone[PT_MAX_DEVICES] = {};
+    bool band_copy = false;                        // the host copy split over the shards (pt_trace)
 };
 Multi M;
 
@@ -2563,6 +2568,15 @@ int multi_setup() {
             ShardScope sc(p);
             RC(dalloc(&M.recv[k], bytes / sizeof(float)));
         }
+    }
+    // the host copy of single-frame calls split over the shards' own links: by default only when
+    // every shard has a device of its own (shards sharing a device share its link, and the split
+    // then only adds the helper hand-offs: tools/multi_probe.py on one GPU)
+    {
+        bool distinct = true;
+        for (int a = 0; a < M.n; ++a)
+            for (int b = a + 1; b < M.n; ++b) distinct = distinct && M.shard[a]->device != M.shard[b]->device;
+        M.band_copy = p->tune.band_copy > 0 || (p->tune.band_copy < 0 && distinct);
     }
     if (M.combine != PT_COMBINE_RCCL) return PT_OK;
     RC(rccl_open());
@@ -3548,6 +3562,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     // combines as usual (the host copy reads the combined image, so it waits for the combine)
     const bool spec = spec_enabled() && (host_image != nullptr || gp->spec_iter == iteration);
     const bool single = M.n <= 1;
+    const bool bands_on = !single && M.band_copy && host_image;
     bool adopted = false;
     const int sum_idx = gp->spec_sum_idx;   // the taken-over frame's image, before the next launch flips it
     BandCopy bands[PT_MAX_DEVICES];
@@ -3558,11 +3573,11 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
             const float* sum = gp->d_spec_sum[gp->spec_sum_idx];
             RC(spec_adopt(host_image != nullptr && single));   // traced already, during the previous call's copy
             // several devices: this shard's bands of the finished sum (the speculative stream has it)
-            if (!single && host_image) RC(band_prepare(bands[k], host_image, sum, gp->spec_stream));
+            if (bands_on) RC(band_prepare(bands[k], host_image, sum, gp->spec_stream));
         } else {
             RC(spec_cancel());
             RC(run_frame(iteration));
-            if (!single && host_image) RC(band_prepare(bands[k], host_image, gp->d_image, gp->stream));
+            if (bands_on) RC(band_prepare(bands[k], host_image, gp->d_image, gp->stream));
         }
         if (g_primary.traced_depth) RC(frame_depth_enqueue());   // read after the one sync below
     }
@@ -3575,7 +3590,7 @@ int32_t pt_trace(pt_uchar4* pbo, int32_t frame, int32_t iteration, float* host_i
     // the next frame, on the second stream, while this one's image is copied out (queued before
     // the copy: a copy into pageable memory may hold the host until it is done)
     if (spec && host_image && iteration < INT32_MAX) RC(spec_launch(iteration + 1));
-    if (host_image && !single) {
+    if (bands_on) {
         // every shard's row bands from its own device, side by side (shard 0's on this thread)
         for (int k = 1; k < nshards(); ++k) g_copy_helpers[k].post(bands[k]);
         hipError_t e = bands[0].run();

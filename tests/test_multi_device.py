@@ -92,10 +92,14 @@ MULTI_CASES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("band_copy", ["-1", "1"])
 @pytest.mark.parametrize("name,res,devices,combine,opts", MULTI_CASES)
-def test_multi_device_api_frames_bitexact(name, res, devices, combine, opts, oracle, ptamd):
+def test_multi_device_api_frames_bitexact(name, res, devices, combine, opts, band_copy, oracle, ptamd, monkeypatch):
     """pathtrace() as main.cpp calls it (one frame per call, host image copied every call, a PBO),
-    split over shard contexts: image, PBO, live counts and TracedDepth equal the oracle's."""
+    split over shard contexts: image, PBO, live counts and TracedDepth equal the oracle's.
+    PT_BAND_COPY=1: the host copy split over the shards' row bands (by default only when every
+    shard has a GPU of its own, which the one-GPU box never has)."""
+    monkeypatch.setenv("PT_BAND_COPY", band_copy)
     a, b = _pair(oracle, ptamd, name, res, 12 if "khaslana" in name else None)
     td = ctypes.c_int32(-7)
     ptamd.lib.pt_init_data_container(ctypes.byref(td))

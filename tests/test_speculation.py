@@ -50,9 +50,12 @@ def _check_frame(tr, r, a, it, td):
     ("cornell_glass_test", (64, 48), {"material_sort": 1, "devices": [0, 0, 0], "combine": "rccl"}),
     ("cornell_obj_bnnuy", (64, 64), {"devices": [0, 0, 0], "combine": "rccl"}),
     ("cornell_obj_bnnuy", (64, 64), {"devices": [0, 0, 0, 0]}),
+    ("cornell_glass_test", (64, 61), {"devices": [0, 0, 0], "band_copy": "1"}),   # host copy by row bands
 ])
 def test_speculated_api_frames_bitexact(name, res, opts, oracle, ptamd, monkeypatch):
     monkeypatch.delenv("PT_SPECULATE", raising=False)
+    opts = dict(opts)
+    monkeypatch.setenv("PT_BAND_COPY", opts.pop("band_copy", "-1"))
     a, b = _pair(oracle, ptamd, name, res)
     td = ctypes.c_int32(-7)
     ptamd.lib.pt_init_data_container(ctypes.byref(td))

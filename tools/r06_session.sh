@@ -28,6 +28,7 @@ for s in "$@"; do
         smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench_k20 400 python bench.py --steps 20 --warmup 5 ;;
         benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
+        bandprobe) step band_probe 200 python tools/band_copy_probe.py ;;
         multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
         multidirect) PT_MULTI_F1_DIRECT=1 step multi_probe_direct 300 python tools/multi_probe.py 20 ;;
         inproc) step inproc 200 python bench.py --gpus 2 --inproc --inproc-devices 0,0 --steps 20 --warmup 5 ;;
