@@ -1137,7 +1137,7 @@ constexpr int64_t AUTO_BATCH_PATHS = 84000000;
 
 // Tuning and test knobs (tools, A/B runs, tests).  Every one is read from the environment in ONE
 // place, read_tuning(), when pt_init builds a context -- never on a hot call -- and none changes a
-// result (the tests run each one against the oracle).  INTEGRATION.md §5 lists them.
+// result (the tests run each one against the oracle).  INTEGRATION.md §4 lists them.
 struct Tuning {
     size_t bounce_lds_pad = 0, bvh_lds_pad = 0;   // PT_BOUNCE_LDS_PAD / PT_BVH_LDS_PAD: unused LDS (occupancy A/B)
     bool sections_skip_camera = false;              // PT_SECTIONS_SKIP_CAMERA: camera bounce out of the counters
