@@ -28,6 +28,18 @@ for s in "$@"; do
         smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench_k20 400 python bench.py --steps 20 --warmup 5 ;;
         benchq) step bench_q 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-api --no-spread ;;
+        calib) step calib_plain 120 project3-cuda-path-tracer-2025_amd/build/fetch_calib
+            step calib_pmc 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/calib -o run --output-format csv -- project3-cuda-path-tracer-2025_amd/build/fetch_calib
+            step calib_pmc_hit 120 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/calib_hit -o run --output-format csv -- project3-cuda-path-tracer-2025_amd/build/fetch_calib ;;
+        calibreq) step calib_req 120 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum -d gpurun_out/calib_req -o run --output-format csv -- project3-cuda-path-tracer-2025_amd/build/fetch_calib
+            step calib_bubble 120 rocprofv3 --kernel-trace --pmc TCC_BUBBLE_sum WRITE_SIZE -d gpurun_out/calib_bubble -o run --output-format csv -- project3-cuda-path-tracer-2025_amd/build/fetch_calib ;;
+        meshreq) R="TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum"
+            PMC_TAG=req_fused_ PMC_SETS="$R" step pmc_req_fused 300 bash tools/pmc.sh
+            PMC_TAG=req_bunny_ PMC_SETS="$R" step pmc_req_bunny 300 bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json
+            PMC_TAG=req_kh_ PMC_STEPS=8 PMC_WARMUP=2 PMC_SETS="$R" step pmc_req_kh 300 bash tools/pmc.sh --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
+            PMC_TAG=req_cyr_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="$R" step pmc_req_cyr 300 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json ;;
+        cyrhit) PMC_TAG=cyrhit_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="TCC_HIT_sum,TCC_MISS_sum" step pmc_cyr_hit 300 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json
+            PMC_TAG=bunhit_ PMC_SETS="TCC_HIT_sum,TCC_MISS_sum" step pmc_bunny_hit 300 bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json ;;
         bandprobe) step band_probe 200 python tools/band_copy_probe.py ;;
         multi) step multi_probe 300 python tools/multi_probe.py 20 ;;
         multidirect) PT_MULTI_F1_DIRECT=1 step multi_probe_direct 300 python tools/multi_probe.py 20 ;;
