@@ -1155,6 +1155,8 @@ struct Tuning {
     bool combine_force_staged = false;              // PT_COMBINE_FORCE_STAGED=1: peer shards via packed tiles
     bool bvh_tree_ref = false;                      // PT_BVH_TREE=ref: the reference's hierarchy, no SAH tree
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
+    int bvh_max_height = -1;                        // PT_BVH_MAX_HEIGHT: SAH tree height bound (0: none; -1: the
+                                                    // height whose LDS stack still admits BVH_WAVES blocks per CU)
     int bvh_bfs_levels = 12;                        // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
                                                     // this many levels, each subtree below in preorder
                                                     // (A/B: 262k -1.0 %, 1.0M -1.4 %, bunny +-0 vs all
@@ -1190,6 +1192,7 @@ Tuning read_tuning() {
     t.bvh_tree_ref = tree && strcmp(tree, "ref") == 0;
     t.bvh_tree_info = getenv("PT_BVH_TREE_INFO") != nullptr;
     t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 12));
+    t.bvh_max_height = (int)std::max(-1L, num("PT_BVH_MAX_HEIGHT", -1));
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
     t.band_copy = (int)std::max(-1L, std::min(1L, num("PT_BAND_COPY", -1)));
@@ -3205,7 +3208,15 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         lhi[3 * k] = nd.hi.x; lhi[3 * k + 1] = nd.hi.y; lhi[3 * k + 2] = nd.hi.z;
                         ls[k] = node_aux[leaf_nodes[k]].y;
                     }
-                    sah = pth::build_sah_tree(llo, lhi, ls, tt, th, gp->tune.bvh_bfs_levels) && th + 1 <= MAXSTACK &&
+                    // the traversal kernels keep one stack entry per tree level in LDS (BLOCK x 4 B each):
+                    // a tree of height h needs (h + 1) KB per block, so the height is bounded to what
+                    // still lets BVH_WAVES blocks share a CU's 160 KB (21 levels; the 262k / 1.0M
+                    // stand-ins' SAH trees are 24 / 26 high unbounded: 6 / 5 blocks)
+                    const int hmax = gp->tune.bvh_max_height > 0 ? gp->tune.bvh_max_height
+                                     : gp->tune.bvh_max_height == 0
+                                         ? (1 << 30)
+                                         : (int)(163840 / ((size_t)BVH_WAVES * BLOCK * sizeof(int))) - 1;
+                    sah = pth::build_sah_tree(llo, lhi, ls, tt, th, gp->tune.bvh_bfs_levels, hmax) && th + 1 <= MAXSTACK &&
                           (int64_t)tt.size() + L < (1 << 24);
                     if (sah) {   // the union of the leaves is the reference root box, bit for bit
                         const pth::TravChild& a = tt[0].c[0];

@@ -86,10 +86,25 @@ static int check_scene(const char* path) {
         }
         if (seen != tree.size()) orders_equal = 0;
     }
+    if (sah && s.size() > 20000) orders_equal = -2;   // not checked
+    // the tightest height bound (1 + ceil(log2 leaves)): every leaf still in the tree exactly once
+    int tight = -1, tight_leaves = 0;
+    if (sah) {
+        std::vector<pth::TravInner> t3;
+        int h3 = 0;
+        if (pth::build_sah_tree(lo, hi, s, t3, h3, 1 << 30, 1)) {
+            tight = h3;
+            std::vector<int> seen(s.size(), 0);
+            for (const pth::TravInner& t : t3)
+                for (const pth::TravChild& c : t.c)
+                    if (c.leaf && c.ref >= 0 && c.ref < (int)s.size()) seen[c.ref]++;
+            for (int x : seen) tight_leaves += x == 1;
+        }
+    }
     std::printf("scene rc=0 geoms=%d materials=%d triangles=%d nodes=%d depth=%d textures=%d bad_tex=%d sah=%d "
-                "sah_orders_equal=%d\n",
+                "sah_orders_equal=%d sah_tight=%d leaves=%zu tight_leaves=%d\n",
                 v.num_geoms, v.num_materials, v.num_triangles, v.num_bvh_nodes, depth, v.num_textures, bad_tex,
-                sah ? height : -1, orders_equal);
+                sah ? height : -1, orders_equal, tight, s.size(), tight_leaves);
     pt_scene_free(f);
     return 0;
 }

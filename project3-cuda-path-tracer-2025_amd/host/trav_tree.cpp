@@ -37,10 +37,17 @@ struct Tmp {
     float s;
 };
 
+int ceil_log2(int c) {
+    int h = 0;
+    while ((1 << h) < c) ++h;
+    return h;
+}
+
 }  // namespace
 
 bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>& leaf_hi,
-                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height, int bfs_levels) {
+                    const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height, int bfs_levels,
+                    int max_height) {
     const int n = (int)leaf_s.size();
     out.clear();
     height = 0;
@@ -57,6 +64,7 @@ bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>&
     struct Work {
         int begin, end, parent, side, depth;
     };
+    max_height = std::max(max_height, 1 + ceil_log2(n));
     std::vector<Work> st{{0, n, -1, 0, 1}};
     while (!st.empty()) {
         const Work w = st.back();
@@ -120,6 +128,18 @@ bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>&
                 };
                 mid = (int)(std::stable_partition(idx.begin() + w.begin, idx.begin() + w.end, left) - idx.begin());
                 if (mid == w.begin || mid == w.end) mid = w.begin + (w.end - w.begin) / 2;
+            }
+            // height bound: a child of c leaves needs ceil(log2 c) more levels at best; a split that
+            // leaves a child no room becomes the median split on the same axis (by centroid, ties by
+            // leaf id), which keeps every subtree within the bound from here on
+            const int big = std::max(mid - w.begin, w.end - mid);
+            if (w.depth + 1 + ceil_log2(big) > max_height) {
+                const int a = bax >= 0 ? bax : 0;
+                mid = w.begin + (w.end - w.begin) / 2;
+                std::nth_element(idx.begin() + w.begin, idx.begin() + mid, idx.begin() + w.end, [&](int x, int y) {
+                    const double cx = cen[3 * (size_t)x + a], cy = cen[3 * (size_t)y + a];
+                    return cx < cy || (cx == cy && x < y);
+                });
             }
             code = (int)T.size();
             T.push_back(Tmp{});

@@ -31,9 +31,12 @@ struct TravInner {
 // throughout, 0: preorder throughout); the root is inner node 0 (n >= 2).  `height`: levels of
 // inner nodes plus the leaf level.  Returns false for n < 2 or for a box with a NaN / infinite
 // coordinate (the containment argument needs ordered, finite bounds): the caller keeps the
-// reference hierarchy.
+// reference hierarchy.  `max_height` bounds `height`: where a SAH split would leave a child no room
+// for a balanced subtree below the bound, the split is the median one (the traversal stack, one
+// entry per level, lives in LDS, whose size sets the traversal kernels' occupancy); a bound below
+// 1 + ceil(log2 n) is raised to it.
 bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>& leaf_hi,
                     const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height,
-                    int bfs_levels = 1 << 30);
+                    int bfs_levels = 1 << 30, int max_height = 1 << 30);
 
 }  // namespace pth

@@ -173,3 +173,24 @@ def test_pair_numbering_does_not_change_results(levels, oracle, ptamd, monkeypat
         assert _eq(tr.image(), r.image), levels
     finally:
         tr.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bound", [0, 19])
+def test_bounded_tree_height_does_not_change_results(bound, oracle, ptamd, monkeypatch):
+    """PT_BVH_MAX_HEIGHT: the SAH tree over the reference's leaves with its height bounded (median
+    splits where SAH would leave a child no room; 0: unbounded) -- the same leaves are visited, so
+    the image is the oracle's."""
+    monkeypatch.setenv("PT_BVH_MAX_HEIGHT", str(bound))
+    name, res = LARGE[1]
+    a = oracle.load_scene(scene_path(name), res=res)
+    b = ptamd.SceneFile(scene_path(name), res=res)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr = ptamd.PathTracer(b)
+    try:
+        for it in range(1, 4):
+            r.trace(it)
+        tr.trace_frames(1, 3)
+        assert _eq(tr.image(), r.image), bound
+    finally:
+        tr.free()

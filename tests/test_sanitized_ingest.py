@@ -80,6 +80,11 @@ def test_every_repository_scene_and_texture(driver):
     # the SAH traversal tree is the same tree under every pair numbering (PT_BVH_BFS_LEVELS)
     for n in ("cornell_obj_bnnuy.json", "cornell_obj_khaslana.json"):
         assert "sah_orders_equal=1" in res[n], (n, res[n])
+        # the height bound at its tightest, 1 + ceil(log2 leaves), still holds every leaf once
+        kv = dict(x.split("=") for x in res[n].split() if "=" in x)
+        leaves = int(kv["leaves"])
+        assert int(kv["sah_tight"]) == 1 + (leaves - 1).bit_length(), (n, res[n])
+        assert int(kv["tight_leaves"]) == leaves, (n, res[n])
     pngs = sorted(glob.glob(os.path.join(REPO, "scenes", "textures", "*.png")) +
                   glob.glob(os.path.join(GOLDEN, "*.png")))
     if pngs:

@@ -75,6 +75,10 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        heightab) ARMS="${HEIGHT_ARMS:-PT_BVH_MAX_HEIGHT=0 - PT_BVH_MAX_HEIGHT=19}"
+            AB_ROUNDS=2 AB_TAG=height_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_height_cyrene 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=height_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_height_phainon 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=height_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 32 --warmup 2" step ab_height_khaslana 900 bash tools/ab_env.sh ;;
         orderab) ARMS="${ORDER_ARMS:-- PT_BVH_BFS_LEVELS=0 PT_BVH_BFS_LEVELS=8 PT_BVH_BFS_LEVELS=12}"
             AB_ROUNDS=2 AB_TAG=order_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_order_cyrene 900 bash tools/ab_env.sh
             AB_ROUNDS=2 AB_TAG=order_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_order_phainon 900 bash tools/ab_env.sh
