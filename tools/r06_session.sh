@@ -75,6 +75,16 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        tpab) L=$PWD/project3-cuda-path-tracer-2025_amd/build/ab
+            ARMS="PTAMD_LIB=$L/tp0.so -"
+            AB_ROUNDS=3 AB_TAG=tp_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_tp_bunny 900 bash tools/ab_env.sh
+            AB_ROUNDS=3 AB_TAG=tp_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 32 --warmup 2" step ab_tp_khaslana 900 bash tools/ab_env.sh
+            AB_ROUNDS=3 AB_TAG=tp_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_tp_cyrene 900 bash tools/ab_env.sh ;;
+        tptraffic) PMC_TAG=tpbun_ PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_tp_bunny 300 bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json
+            PMTAG=x PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/tp0.so PMC_TAG=tp0bun_ PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_tp0_bunny 300 bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json ;;
+        cyrmix) IM="SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_SMEM,SQ_INSTS_VMEM,SQ_WAVE_CYCLES;SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_WAIT_INST_ANY,GRBM_GUI_ACTIVE,TA_BUSY_avr,TA_TA_BUSY_sum"
+            PMC_TAG=imcyr_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="$IM" step pmc_mix_cyr 300 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json
+            PMC_TAG=imbun_ PMC_SETS="$IM" step pmc_mix_bunny 300 bash tools/pmc.sh --scene scenes/cornell_obj_bnnuy.json ;;
         heightab) ARMS="${HEIGHT_ARMS:-PT_BVH_MAX_HEIGHT=0 - PT_BVH_MAX_HEIGHT=19}"
             AB_ROUNDS=2 AB_TAG=height_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_height_cyrene 900 bash tools/ab_env.sh
             AB_ROUNDS=2 AB_TAG=height_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_height_phainon 900 bash tools/ab_env.sh
