@@ -71,6 +71,10 @@ struct SceneDev {
     int num_textures;
     // VAR_BVH_FAST layout (pairs != null when the tree allows it, see DevPair)
     const DevPair* pairs;
+    // 4-wide layout of the same hierarchy (trav_inner4, trees past the L2; null: pairs only):
+    // num_quads records of 8 float4 = one 128-B line each, leaves referenced as num_quads + leaf
+    const float4* quads;
+    int num_quads;
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
@@ -587,13 +591,66 @@ PT_DEV void trav_leaf(const SceneDev& sc, TravState& st, int leaf, int& n_nodes,
         }
     }
 }
-// one node expansion or one leaf; st.cur < 0 afterwards: the ray is finished
+// 4-wide node (SceneDev::quads): up to four children of the same hierarchy -- a pair's children,
+// or for an inner child its own two children (two levels in one record) -- in ONE 128-B line:
+// float4 [0..2] lo.x / lo.y / lo.z of children 0..3, [3..5] hi.x / hi.y / hi.z, [6] refs (int
+// bits, -1: no child), [7] cull constants (pack_cull).  Every passing, not culled child is kept:
+// the nearest continues, the others are pushed farthest first (so they pop nearest first).  Box
+// decisions and culls are trav_inner's, child by child, so the visited leaves are the same.
 template <bool COUNT = false>
+PT_DEV bool trav_inner4(const SceneDev& sc, TravState& st, int* stack, int& n_nodes) {
+    const float t_best = st.t_hit;
+    if (COUNT) n_nodes++;
+    const v4f* Q = reinterpret_cast<const v4f*>(sc.quads) + 8 * (size_t)st.cur;
+    v4f q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = Q[k];
+    float key[4], T[4];
+    int ref[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 lo = make_float4(q[0][i], q[1][i], q[2][i], 0.f);
+        const float4 hi = make_float4(q[3][i], q[4][i], q[5][i], 0.f);
+        ref[i] = __float_as_int(q[6][i]);
+        float e = 0.f;
+        bool p;
+        if (st.wfast) {   // wave-uniform
+            bool amb;
+            p = aabb_fast(lo, hi, st.ro, st.rr, e, amb);
+            if (amb && ref[i] >= 0) p = aabb_test(lo, hi, st.ro, st.rd);   // rare: the reference decides
+        } else {
+            p = aabb_decide(lo, hi, st.ro, st.rd, st.rr, st.exact, e);
+        }
+        T[i] = cull_threshold_packed(e, q[7][i]);
+        p = p && ref[i] >= 0 && !(t_best < T[i]);
+        key[i] = p ? e : __builtin_inff();
+    }
+    // order the four by entry (a network of five compare-exchanges; failed children last)
+    auto cx = [&](int a, int b) {
+        if (key[b] < key[a]) {
+            float tk = key[a]; key[a] = key[b]; key[b] = tk;
+            float tt = T[a]; T[a] = T[b]; T[b] = tt;
+            int tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;
+        }
+    };
+    cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+    if (!(key[0] < __builtin_inff())) return false;    // no child passes: the caller pops
+    const int S = sc.ref_shift;
+#pragma unroll
+    for (int i = 3; i >= 1; --i)
+        if (key[i] < __builtin_inff() && st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(ref[i], T[i], S);
+    st.cur = ref[0];
+    st.curT = T[0];
+    return true;
+}
+
+// one node expansion or one leaf; st.cur < 0 afterwards: the ray is finished
+template <bool COUNT = false, bool QUAD = false>
 PT_DEV void trav_step(const SceneDev& sc, TravState& st, int* stack, int& n_nodes, int& n_tris) {
-    const int P = sc.num_pairs;
+    const int P = QUAD ? sc.num_quads : sc.num_pairs;
     bool next = false;
     if (st.cur < P) {
-        next = trav_inner<COUNT>(sc, st, stack, n_nodes);
+        next = QUAD ? trav_inner4<COUNT>(sc, st, stack, n_nodes) : trav_inner<COUNT>(sc, st, stack, n_nodes);
     } else {
         trav_leaf<COUNT>(sc, st, st.cur - P, n_nodes, n_tris);
     }
@@ -634,7 +691,7 @@ PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node) {
 // `defer` lanes of the wave are still traversing: those stop with st.cur >= 0 (wave steps with a
 // handful of lanes cost a wave slot each for a few lanes of work; k_bvh_tail_trav resumes them in
 // full waves).  Counters (COUNT) as bvh_intersect_pairs', the per-ray ones left to the caller.
-template <bool COUNT = false>
+template <bool COUNT = false, bool QUAD = false>
 PT_DEV void trav_run(const SceneDev& sc, TravState& st, int* stack, int defer, int& n_nodes, int& n_tris,
                      int hist = SEC_BVH_LANES_HIST) {
     while (st.cur >= 0) {
@@ -644,7 +701,7 @@ PT_DEV void trav_run(const SceneDev& sc, TravState& st, int* stack, int defer, i
             sec_add(SEC_N_BVH_WITERS, 1);
             sec_add(hist + (lanes - 1) / 4, 1);
         }
-        trav_step<COUNT>(sc, st, stack, n_nodes, n_tris);
+        trav_step<COUNT, QUAD>(sc, st, stack, n_nodes, n_tris);
     }
 }
 

@@ -591,7 +591,7 @@ PT_DEV bool tail_put(const TailBuf& t, int* ctr, int seg, int qs, const TravStat
     return true;
 }
 
-template <int VAR>
+template <int VAR, bool QUAD>
 __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, QueueBuf q, TailBuf tail, int defer,
                                                                  PathBuf out, FrameCtl* ctl, float* __restrict__ image,
                                                                  int bounce, int seg_stride) {
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
         if (CNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
         // handed over: the wave's last few traversals go on 64 to a wave (no room: finish here)
         for (int d = defer;; d = 0) {
-            trav_run<CNT>(sc, st, s_stack + tid, d, n_nodes, n_tris);
+            trav_run<CNT, QUAD>(sc, st, s_stack + tid, d, n_nodes, n_tris);
             if (st.cur < 0) break;
             if (tail_put(tail, &ctl->qcnt[bounce][seg][1], seg, qs, st, s_stack + tid)) {
                 handed = true;
@@ -657,7 +657,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
 // refill), so a wave drains once, when its segment is done, instead of once per 64 rays.
 // Traversal only: a finished ray's result (t, u, v, triangle) replaces its saved hit, and
 // k_bvh_tail_shade shades the entries in full waves.  No barrier: waves leave on their own.
-template <int VAR>
+template <int VAR, bool QUAD>
 __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc, QueueBuf q, TailBuf t, FrameCtl* ctl,
                                                                     int bounce, int refill) {
     extern __shared__ float4 s_dyn[];
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
                 sec_add(SEC_N_BVH_WITERS, 1);
                 sec_add(SEC_TAIL_LANES_HIST + (lanes - 1) / 4, 1);
             }
-            trav_step<CNT>(sc, st, s_stack, n_nodes, n_tris);
+            trav_step<CNT, QUAD>(sc, st, s_stack, n_nodes, n_tris);
             if (st.cur < 0) {
                 t.hit[e] = trav_saved_hit(st);
                 if (CNT) {
@@ -1157,6 +1157,9 @@ struct Tuning {
     bool bvh_tree_info = false;                     // PT_BVH_TREE_INFO: print the traversal tree's shape
     int bvh_max_height = -1;                        // PT_BVH_MAX_HEIGHT: SAH tree height bound (0: none; -1: the
                                                     // height whose LDS stack still admits BVH_WAVES blocks per CU)
+    int bvh_quad = 1;                               // PT_BVH_QUAD: the traversal kernels on 4-wide records (1) or on
+                                                    // the pairs (0) (A/B: 262k -7.6 %, 1.0M -8.7 %, bunny -5.0 %,
+                                                    // khaslana -1.9 %; profiles/r06_ab_four_wide.json)
     int bvh_bfs_levels = 12;                        // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
                                                     // this many levels, each subtree below in preorder
                                                     // (A/B: 262k -1.0 %, 1.0M -1.4 %, bunny +-0 vs all
@@ -1193,6 +1196,7 @@ Tuning read_tuning() {
     t.bvh_tree_info = getenv("PT_BVH_TREE_INFO") != nullptr;
     t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 12));
     t.bvh_max_height = (int)std::max(-1L, num("PT_BVH_MAX_HEIGHT", -1));
+    t.bvh_quad = num("PT_BVH_QUAD", 1) != 0 ? 1 : 0;
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
     t.band_copy = (int)std::max(-1L, std::min(1L, num("PT_BAND_COPY", -1)));
@@ -1225,6 +1229,7 @@ struct State {
     DevNode* d_nodes = nullptr;
     DevTriHot* d_hot = nullptr;
     DevPair* d_pairs = nullptr;
+    float4* d_quads = nullptr;       // the 4-wide layout (SceneDev::quads), trees past the L2
     DevTriHot* d_hot4 = nullptr;
     float4* d_leaf9 = nullptr;
     DevTriCold* d_cold = nullptr;
@@ -1396,11 +1401,19 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
         const size_t stack_bytes = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int);
         // the handed-over stacks were sized for the pair tree of the allocation (ensure_frames)
         if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
-        launch(200 + b, k_bvh_bounce<VAR>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue, gp->tail,
-               gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
+        if (gp->sc.quads)   // the 4-wide layout (trees past the L2)
+            launch(200 + b, k_bvh_bounce<VAR, true>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue,
+                   gp->tail, gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
+        else
+            launch(200 + b, k_bvh_bounce<VAR, false>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue,
+                   gp->tail, gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
         if (gp->tail_lanes > 0) {   // the handed-over rays: refilling waves, then their shading
-            launch(400 + b, k_bvh_tail_trav<VAR>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes, gp->sc,
-                   gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
+            if (gp->sc.quads)
+                launch(400 + b, k_bvh_tail_trav<VAR, true>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes,
+                       gp->sc, gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
+            else
+                launch(400 + b, k_bvh_tail_trav<VAR, false>, dim3(NSEG * gp->tail_trav_blocks), dim3(BLOCK), stack_bytes,
+                       gp->sc, gp->queue, gp->tail, gp->d_ctl, b, gp->tail_refill);
             const int per_seg = gp->tail_shade_blocks > 0 ? std::min(gp->tail_shade_blocks, nblocks(gp->tail.stride))
                                                           : nblocks(gp->tail.stride);
             launch(400 + b, k_bvh_tail_shade<VAR>, dim3(NSEG * per_seg), dim3(BLOCK), 0, gp->sc,
@@ -2314,7 +2327,7 @@ void free_all() {
     gp->band_ready = nullptr;
     release_graph();
     free_pass_buffers();
-    void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_hot4,
+    void* ptrs[] = {gp->d_geoms, gp->d_cull, gp->d_mats, gp->d_nodes, gp->d_node_aux, gp->d_hot, gp->d_pairs, gp->d_quads, gp->d_hot4,
                     gp->d_leaf9, gp->d_cold, gp->d_texels, gp->d_texinfo, gp->d_image, gp->d_ctl, gp->d_grid};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -2970,6 +2983,8 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     std::vector<DevTriHot> hot;
     std::vector<DevTriCold> cold;
     std::vector<DevPair> pairs;      // VAR_BVH_FAST layout (empty: tree not representable)
+    std::vector<float4> quads;       // its 4-wide form (8 float4 per record; empty: not built)
+    int quad_stack = 0;              // stack entries the 4-wide traversal can need
     std::vector<DevTriHot> hot4;
     std::vector<float4> leaf9;
     int pair_root_ref = 0, pair_count = 0, pair_ref_shift = 16;
@@ -3245,6 +3260,92 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                     }
                     gp->stack_depth = std::max(gp->stack_depth, th + 1);
                     gp->pair_depth = th + 1;
+                    // the 4-wide form of the same hierarchy: record q holds the children of binary
+                    // node n, an inner child replaced by its own two children (two levels per
+                    // record, one 128-B line); quad 0 is the root's.  Inner refs breadth-first over
+                    // the top levels, preorder below, as the pairs (PT_BVH_BFS_LEVELS / 2 levels).
+                    const bool quad_on = gp->tune.bvh_quad > 0;
+                    if (quad_on) {
+                        // children of the record for binary node n (TravChild: leaf -> itself,
+                        // inner -> its two children)
+                        auto kids = [&](int n, pth::TravChild* out) {
+                            int k = 0;
+                            for (int c = 0; c < 2; ++c) {
+                                const pth::TravChild& ch = tt[n].c[c];
+                                if (ch.leaf) out[k++] = ch;
+                                else { out[k++] = tt[ch.ref].c[0]; out[k++] = tt[ch.ref].c[1]; }
+                            }
+                            return k;
+                        };
+                        // the binary nodes that head a record: the root and every inner grandchild
+                        // reached through an inner child, or inner child of ... (every inner kid)
+                        std::vector<int> qnode{0}, qdepth{0};
+                        std::vector<int> qid(P, -1);
+                        qid[0] = 0;
+                        for (size_t h = 0; h < qnode.size(); ++h) {   // breadth-first
+                            pth::TravChild k4[4];
+                            const int nk = kids(qnode[h], k4);
+                            for (int i = 0; i < nk; ++i)
+                                if (!k4[i].leaf) {
+                                    qid[k4[i].ref] = (int)qnode.size();
+                                    qnode.push_back(k4[i].ref);
+                                    qdepth.push_back(qdepth[h] + 1);
+                                }
+                        }
+                        const int Q = (int)qnode.size();
+                        // numbering: breadth-first over the top levels, each subtree below in preorder
+                        const int qlev = std::max(0, gp->tune.bvh_bfs_levels / 2);
+                        std::vector<int> order, num(Q, -1);
+                        std::vector<int> roots;
+                        for (int h = 0; h < Q; ++h) {
+                            if (qdepth[h] < qlev) order.push_back(h);
+                            else if (qdepth[h] == qlev) roots.push_back(h);
+                        }
+                        for (int r : roots) {
+                            std::vector<int> st{r};
+                            while (!st.empty()) {
+                                const int h = st.back();
+                                st.pop_back();
+                                order.push_back(h);
+                                pth::TravChild k4[4];
+                                const int nk = kids(qnode[h], k4);
+                                for (int i = nk - 1; i >= 0; --i)
+                                    if (!k4[i].leaf) st.push_back(qid[k4[i].ref]);
+                            }
+                        }
+                        for (int i = 0; i < (int)order.size(); ++i) num[order[i]] = i;
+                        quads.assign(8 * (size_t)Q, make_float4(0.f, 0.f, 0.f, 0.f));
+                        std::vector<int> need(Q, 0);   // stack entries below record h (children - 1 per level)
+                        for (int h = Q - 1; h >= 0; --h) {   // children after parents in breadth-first order
+                            pth::TravChild k4[4];
+                            const int nk = kids(qnode[h], k4);
+                            float4* R = &quads[8 * (size_t)num[h]];
+                            int deeper = 0;
+                            for (int i = 0; i < 4; ++i) {
+                                float* f[8] = {&R[0].x, &R[1].x, &R[2].x, &R[3].x, &R[4].x, &R[5].x, &R[6].x, &R[7].x};
+                                if (i < nk) {
+                                    const pth::TravChild& c = k4[i];
+                                    for (int a = 0; a < 3; ++a) {
+                                        f[a][i] = c.lo[a];
+                                        f[3 + a][i] = c.hi[a];
+                                    }
+                                    const int rf = c.leaf ? Q + c.ref : num[qid[c.ref]];
+                                    memcpy(&f[6][i], &rf, 4);
+                                    f[7][i] = pack_cull(c.s);
+                                    if (!c.leaf) deeper = std::max(deeper, need[qid[c.ref]]);
+                                } else {
+                                    const int none = -1;
+                                    memcpy(&f[6][i], &none, 4);
+                                }
+                            }
+                            need[h] = (nk - 1) + deeper;
+                        }
+                        quad_stack = need[0] + 1;
+                        gp->stack_depth = std::max(gp->stack_depth, quad_stack);
+                        gp->pair_depth = std::max(gp->pair_depth, quad_stack);   // the push bound covers both
+                        if (gp->tune.bvh_tree_info)
+                            fprintf(stderr, "pt_init: 4-wide records %d (pairs %d), stack %d entries\n", Q, P, quad_stack);
+                    }
                     if (gp->tune.bvh_tree_info)
                         fprintf(stderr, "pt_init: SAH traversal tree over %d reference leaves, height %d (reference %d)\n", L,
                                 th, height);
@@ -3376,6 +3477,10 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
             RC(upload(gp->d_hot4, hot4.data(), hot4.size()));
             RC(dalloc(&gp->d_leaf9, leaf9.size()));
             RC(upload(gp->d_leaf9, leaf9.data(), leaf9.size()));
+            if (!quads.empty()) {
+                RC(dalloc(&gp->d_quads, quads.size()));
+                RC(upload(gp->d_quads, quads.data(), quads.size()));
+            }
         }
     }
     // textures (pathtrace.cu:169-201): RGBA8 texels of every texture in one buffer
@@ -3437,6 +3542,8 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     sc.hot4 = gp->d_hot4;
     sc.leaf9 = gp->d_leaf9;
     sc.num_pairs = pair_count;
+    sc.quads = gp->split ? gp->d_quads : nullptr;   // the 4-wide records serve the traversal kernels only
+    sc.num_quads = (int)(quads.size() / 8);
     sc.root_ref = pair_root_ref;
     sc.ref_shift = pair_ref_shift;
     sc.root_lo = pair_root_lo;

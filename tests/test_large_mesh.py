@@ -194,3 +194,36 @@ def test_bounded_tree_height_does_not_change_results(bound, oracle, ptamd, monke
         assert _eq(tr.image(), r.image), bound
     finally:
         tr.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quad", [0, 1])
+@pytest.mark.parametrize("name,res,depth,lanes", [("cornell_obj_bnnuy", (96, 96), None, 40),
+                                                   ("cornell_obj_khaslana", (64, 64), 12, 56),
+                                                   ("cornell_obj_cyrene", (48, 48), None, 8)])
+def test_four_wide_records_bitexact(name, res, depth, lanes, quad, oracle, ptamd, monkeypatch):
+    """PT_BVH_QUAD: the traversal kernels on 4-wide records (two levels of the hierarchy in one
+    128-B line; by default for trees of 65,536 refs or more) or on the pairs, forced either way on
+    every mesh scene -- multi-frame passes and API frames bit-exact, live counts included."""
+    monkeypatch.setenv("PT_BVH_QUAD", str(quad))
+    monkeypatch.setenv("PT_BVH_TAIL_LANES", str(lanes))
+    a = oracle.load_scene(scene_path(name), res=res, depth=depth)
+    b = ptamd.SceneFile(scene_path(name), res=res, depth=depth)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr = ptamd.PathTracer(b)
+    try:
+        segs = 0
+        for it in range(1, 5):
+            segs += int(np.maximum(r.trace(it), 0).sum())
+        tr.trace_frames(1, 4)
+        st = tr.stats()
+        assert sum(st["queued_total"]) > 0
+        assert _eq(tr.image(), r.image), (name, quad)
+        assert st["segments_total"] == segs
+        for it in (5, 6):
+            live = r.trace(it)
+            tr.trace(it, copy_image=True)
+            assert tr.stats()["live"][:a.trace_depth] == [int(x) if x >= 0 else 0 for x in live][:a.trace_depth]
+        assert _eq(tr.image(), r.image), (name, quad)
+    finally:
+        tr.free()
