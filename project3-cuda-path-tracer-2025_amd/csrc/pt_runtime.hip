@@ -2208,13 +2208,13 @@ int q_stride_for(int frames) {
     return ((nb + NSEG - 1) / NSEG) * BLOCK;
 }
 // k_bvh_bounce hands a wave's traversals to k_bvh_tail_trav once no more than this many of its lanes
-// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56).  By default 40, and 48 for trees
+// are still traversing (PT_BVH_TAIL_LANES, 0: never; at most 56).  By default 32, and 48 for trees
 // of 65,536 refs or more (stack entries with refs wider than 16 bits): deeper traversals diverge
-// more, so handing over earlier pays (A/B, profiles/r06_ab_tail_lanes.json: bunny / khaslana best
-// at 40, within 0.5 % of 32; the 262k / 1.0M-triangle stand-ins best at 48, 2-3 % below 32)
+// more, so handing over earlier pays (A/B on the 4-wide records, profiles/r06_ab_tail_lanes_four_wide.json:
+// bunny / khaslana best at 32, the 262k stand-in at 48, 3.5 % below 32)
 int bvh_tail_lanes() {
     if (gp->tune.bvh_tail_lanes >= 0) return gp->tune.bvh_tail_lanes;
-    return 32 - gp->sc.ref_shift > 16 ? 48 : 40;
+    return 32 - gp->sc.ref_shift > 16 ? 48 : 32;
 }
 // entries per tail segment: what k_bvh_bounce can hand over, `lanes` per wave of its blocks of one
 // segment.  Tools: PT_BVH_TAIL_CHUNKS=c caps it at c blocks' worth; a lane that finds its segment

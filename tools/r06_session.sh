@@ -75,6 +75,13 @@ for s in "$@"; do
         meshstats) B="python bench.py --no-cpu-baseline --no-configs --no-api --no-spread"
             step prof_c4_bunny 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4_bunny -o run --output-format csv -- $B --steps 48 --warmup 4 --scene scenes/cornell_obj_bnnuy.json
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
+        occab) ARMS="- PT_BVH_LDS_PAD=5120 PT_BVH_LDS_PAD=11264"
+            AB_ROUNDS=2 AB_TAG=occ_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_occ_bunny 900 bash tools/ab_env.sh ;;
+        treeinfo) step tree_info 300 python -u tools/tree_info.py ;;
+        quadlanes) ARMS="${LANE_ARMS:-PT_BVH_TAIL_LANES=32 PT_BVH_TAIL_LANES=40 PT_BVH_TAIL_LANES=48 PT_BVH_TAIL_LANES=56}"
+            AB_ROUNDS=2 AB_TAG=qlanes_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_qlanes_bunny 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=qlanes_khaslana AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 --steps 32 --warmup 2" step ab_qlanes_khaslana 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=qlanes_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_qlanes_cyrene 900 bash tools/ab_env.sh ;;
         quadtest) step pytest_quad 600 $PYT tests/test_large_mesh.py -m gpu -k "four_wide" ;;
         quadab) ARMS="${QUAD_ARMS:-PT_BVH_QUAD=0 PT_BVH_QUAD=1}"
             AB_ROUNDS=3 AB_TAG=quad_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_quad_cyrene 900 bash tools/ab_env.sh
