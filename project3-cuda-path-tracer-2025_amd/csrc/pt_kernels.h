@@ -75,6 +75,10 @@ struct SceneDev {
     // num_quads records of 8 float4 = one 128-B line each, leaves referenced as num_quads + leaf
     const float4* quads;
     int num_quads;
+    // traversal stack of the split kernels: entries [0, stack_lds) in the block's LDS, deeper
+    // ones (rare) in `spill`, spill_stride entries per traversal-queue slot (TravState::qs)
+    int stack_lds, spill_stride;
+    int* spill;
     const DevTriHot* hot4;    // 4-slot triangle groups per leaf; slot 0's c.z = count (int bits)
     const float4* leaf9;      // per leaf, 9 float4: v0.x v0.y v0.z e1.x .. e2.z, each over the 4 slots
     int num_pairs, root_ref;
@@ -469,6 +473,7 @@ struct TravState {
     f3 ro, rd, rr;
     float t_hit, bu, bv;   // t_hit starts at t_limit (the primitives' t): see trav_begin
     int btri, cur, sp;
+    int qs;       // traversal-queue slot (the spill area's row; -1: LDS stack only)
     float curT;   // certified cull threshold of st.cur (0: none)
     bool exact;
     bool wfast;   // wave-uniform: every ray of the wave is finite with all |d| >= 1e-5 (aabb_fast)
@@ -494,6 +499,7 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
     st.bu = st.bv = 0.f;
     st.btri = 0x7fffffff;
     st.sp = 0;
+    st.qs = -1;
     st.curT = 0.f;
     float e0;
     st.cur = (aabb_decide(sc.root_lo, sc.root_hi, ro, rd, st.rr, st.exact, e0) &&
@@ -501,13 +507,21 @@ PT_DEV void trav_begin(const SceneDev& sc, TravState& st, f3 ro, f3 rd, float t_
                  ? sc.root_ref
                  : -1;
 }
+// stack entry i of the ray: the block's LDS below sc.stack_lds, its spill row above (split kernels)
+PT_DEV int* trav_slot(const SceneDev& sc, const TravState& st, int* stack, int i) {
+    return (i < sc.stack_lds || st.qs < 0) ? stack + i * BLOCK
+                                           : sc.spill + (size_t)st.qs * sc.spill_stride + (i - sc.stack_lds);
+}
+PT_DEV void trav_push(const SceneDev& sc, TravState& st, int* stack, uint32_t w) {
+    if (st.sp < sc.pair_stack_depth) *trav_slot(sc, st, stack, st.sp++) = (int)w;
+}
 // pop the nearest stack entry whose certified cull does not reject it (st.cur = -1: empty)
 PT_DEV void trav_pop(const SceneDev& sc, TravState& st, int* stack) {
     const float tb = st.t_hit;
     const int S = sc.ref_shift;
     st.cur = -1;
     while (st.sp > 0) {
-        const uint32_t w = (uint32_t)stack[(--st.sp) * BLOCK];
+        const uint32_t w = (uint32_t)*trav_slot(sc, st, stack, --st.sp);
         const float T = unpack_T(w, S);
         if (!(tb < T)) {
             st.cur = (int)(w >> S);
@@ -550,7 +564,7 @@ PT_DEV bool trav_inner(const SceneDev& sc, TravState& st, int* stack, int& n_nod
         st.curT = lfirst ? Tl : Tr;
         const int far = lfirst ? rrf : rl;
         const float Tf = lfirst ? Tr : Tl;
-        if (st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(far, Tf, sc.ref_shift);
+        trav_push(sc, st, stack, pack_ref(far, Tf, sc.ref_shift));
         return true;
     }
     if (pl | pb) {
@@ -638,7 +652,7 @@ PT_DEV bool trav_inner4(const SceneDev& sc, TravState& st, int* stack, int& n_no
     const int S = sc.ref_shift;
 #pragma unroll
     for (int i = 3; i >= 1; --i)
-        if (key[i] < __builtin_inff() && st.sp < sc.pair_stack_depth) stack[(st.sp++) * BLOCK] = (int)pack_ref(ref[i], T[i], S);
+        if (key[i] < __builtin_inff()) trav_push(sc, st, stack, pack_ref(ref[i], T[i], S));
     st.cur = ref[0];
     st.curT = T[0];
     return true;
@@ -677,8 +691,9 @@ PT_DEV float4 trav_saved_hit(const TravState& st) {
 }
 // node to expand next (refs < 2^24) | stack depth (<= MAXSTACK) << 24
 PT_DEV int trav_saved_node(const TravState& st) { return st.cur | (st.sp << 24); }
-PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node) {
+PT_DEV void trav_resume(TravState& st, f3 ro, f3 rd, float4 hit, int node, int qs) {
     trav_ray(st, ro, rd);
+    st.qs = qs;
     st.t_hit = hit.x;
     st.bu = hit.y;
     st.bv = hit.z;

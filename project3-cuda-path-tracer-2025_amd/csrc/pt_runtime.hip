@@ -249,8 +249,8 @@ struct QueueBuf {
 struct TailBuf {
     int2* node;     // queue slot | trav_saved_node
     float4* hit;    // trav_saved_hit
-    int* stack;
-    int stride, cap;
+    int* stack;     // the LDS part of the stack (SceneDev::stack_lds entries; deeper ones stay spilled)
+    int stride, cap, depth;
 };
 // queue entry k for path p and its primitive result
 PT_DEV void queue_put(const QueueBuf& q, int k, const PathReg& p, float qt, int qw, f3 qs) {
@@ -583,7 +583,7 @@ PT_DEV bool tail_put(const TailBuf& t, int* ctr, int seg, int qs, const TravStat
     const int e = seg * t.stride + slot;
     t.node[e] = make_int2(qs, trav_saved_node(st));
     t.hit[e] = trav_saved_hit(st);
-    for (int i = 0; i < st.sp; ++i) t.stack[(size_t)i * t.cap + e] = s_stack[i * BLOCK];
+    for (int i = 0; i < min(st.sp, t.depth); ++i) t.stack[(size_t)i * t.cap + e] = s_stack[i * BLOCK];
     // stats (pt_frame_stats handed_total / handed_stack_total): same-address atomics, one per
     // wave after the compiler's wave reduction, on the counter line the reservation just used
     atomicAdd(ctr + 2, 1);
@@ -625,6 +625,7 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_bounce(SceneDev sc, Qu
         int n_nodes = 0, n_tris = 0;
         TravState st;
         trav_begin(sc, st, p.o, p.d, t_prim);
+        st.qs = qs;   // deep stack entries spill to the slot's row (SceneDev::spill)
         if (CNT) sec_add_lanes(SEC_N_ROOT_CULLED, st.cur < 0 ? 1 : 0);
         // handed over: the wave's last few traversals go on 64 to a wave (no room: finish here)
         for (int d = defer;; d = 0) {
@@ -686,8 +687,9 @@ __global__ __launch_bounds__(BLOCK, BVH_WAVES) void k_bvh_tail_trav(SceneDev sc,
                     const int2 nd = t.node[e];
                     qs = nd.x;
                     const float4 a = q.A[qs], b = q.B[qs];
-                    trav_resume(st, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), t.hit[e], nd.y);
-                    for (int i = 0; i < st.sp; ++i) s_stack[i * BLOCK] = t.stack[(size_t)i * t.cap + e];
+                    trav_resume(st, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), t.hit[e], nd.y, qs);
+                    // the LDS part of its stack (spilled entries stay in the slot's row)
+                    for (int i = 0; i < min(st.sp, sc.stack_lds); ++i) s_stack[i * BLOCK] = t.stack[(size_t)i * t.cap + e];
                     n_nodes = n_tris = 0;
                     if (CNT) {
                         sp0 = st.sp;
@@ -1160,6 +1162,8 @@ struct Tuning {
     int bvh_quad = 1;                               // PT_BVH_QUAD: the traversal kernels on 4-wide records (1) or on
                                                     // the pairs (0) (A/B: 262k -7.6 %, 1.0M -8.7 %, bunny -5.0 %,
                                                     // khaslana -1.9 %; profiles/r06_ab_four_wide.json)
+    int bvh_stack_lds = 0;                          // PT_BVH_STACK_LDS: traversal stack entries kept in LDS by the split
+                                                    // kernels, deeper ones spilled to a row per queue slot (0: all)
     int bvh_bfs_levels = 12;                        // PT_BVH_BFS_LEVELS: SAH pairs numbered breadth-first over
                                                     // this many levels, each subtree below in preorder
                                                     // (A/B: 262k -1.0 %, 1.0M -1.4 %, bunny +-0 vs all
@@ -1197,6 +1201,7 @@ Tuning read_tuning() {
     t.bvh_bfs_levels = (int)std::max(0L, num("PT_BVH_BFS_LEVELS", 12));
     t.bvh_max_height = (int)std::max(-1L, num("PT_BVH_MAX_HEIGHT", -1));
     t.bvh_quad = num("PT_BVH_QUAD", 1) != 0 ? 1 : 0;
+    t.bvh_stack_lds = (int)std::max(0L, num("PT_BVH_STACK_LDS", 0));
     t.grid = (int)num("PT_GRID", -1);
     t.speculate = num("PT_SPECULATE", 1) != 0;
     t.band_copy = (int)std::max(-1L, std::min(1L, num("PT_BAND_COPY", -1)));
@@ -1398,9 +1403,9 @@ void launch_bounce_t(dim3 grid, PathBuf in, PathBuf out, int b) {
            in, out, gp->d_ctl, gp->d_image, b, gp->seg_stride, gp->queue);
     const size_t lds_pad = gp->tune.bvh_lds_pad;
     if (SPLIT) {
-        const size_t stack_bytes = (size_t)gp->sc.pair_stack_depth * BLOCK * sizeof(int);
+        const size_t stack_bytes = (size_t)gp->sc.stack_lds * BLOCK * sizeof(int);
         // the handed-over stacks were sized for the pair tree of the allocation (ensure_frames)
-        if (gp->tail_lanes > 0 && gp->sc.pair_stack_depth > gp->tail_depth) gp->tail_lanes = 0;
+        if (gp->tail_lanes > 0 && gp->sc.stack_lds > gp->tail_depth) gp->tail_lanes = 0;
         if (gp->sc.quads)   // the 4-wide layout (trees past the L2)
             launch(200 + b, k_bvh_bounce<VAR, true>, grid, dim3(BLOCK), stack_bytes + lds_pad, gp->sc, gp->queue,
                    gp->tail, gp->tail_lanes, out, gp->d_ctl, gp->d_image, b, gp->seg_stride);
@@ -2189,6 +2194,7 @@ void free_pass_buffers() {
     dfree(gp->tail.hit);
     dfree(gp->tail.stack);
     gp->tail.stride = gp->tail.cap = 0;
+    dfree(gp->sc.spill);
     dfree(gp->d_contrib);
     gp->sc.contrib = nullptr;
     gp->alloc_frames = 0;
@@ -2235,9 +2241,9 @@ int capacity_for(int frames) {
 size_t pass_bytes(int frames, bool staged) {
     const size_t cap = (size_t)capacity_for(frames);
     size_t b = 2 * 3 * sizeof(float4) * cap;                                     // path ping-pong
-    if (gp->split) b += 4 * sizeof(float4) * (size_t)q_stride_for(frames) * NSEG;   // traversal queue
+    if (gp->split) b += (4 * sizeof(float4) + sizeof(int) * gp->sc.spill_stride) * (size_t)q_stride_for(frames) * NSEG;   // traversal queue (+ stack spill rows)
     if (gp->split && bvh_tail_lanes() > 0)   // handed-over traversals
-        b += (sizeof(int2) + sizeof(float4) + sizeof(int) * std::max(1, gp->sc.pair_stack_depth)) * NSEG *
+        b += (sizeof(int2) + sizeof(float4) + sizeof(int) * std::max(1, gp->sc.stack_lds)) * NSEG *
              (size_t)tail_stride(frames, bvh_tail_lanes());
     if (frames > 1) b += 3 * sizeof(float) * (size_t)gp->pixels_total * frames;      // contribution planes
     if (staged) b += cap * (sizeof(float4) + 3 * sizeof(int) + (gp->num_tex ? 2 * sizeof(float4) : 0));
@@ -2270,11 +2276,14 @@ int ensure_frames(int frames) {
         gp->tail_refill = gp->tune.tail_refill;
         gp->tail_trav_blocks = gp->tune.tail_trav_blocks;
         gp->tail_shade_blocks = gp->tune.tail_shade_blocks;
+        // stack entries past the LDS part: one row per queue slot (rare: deep stacks only)
+        if (gp->sc.spill_stride > 0) RC(dalloc(&gp->sc.spill, qn * (size_t)gp->sc.spill_stride));
         if (gp->tail_lanes > 0) {   // a wave hands over at most tail_lanes rays
-            gp->tail_depth = std::max(1, gp->sc.pair_stack_depth);
+            gp->tail_depth = std::max(1, gp->sc.stack_lds);
             TailBuf& t = gp->tail;
             t.stride = tail_stride(frames, gp->tail_lanes);
             t.cap = t.stride * NSEG;
+            t.depth = gp->tail_depth;
             RC(dalloc(&t.node, (size_t)t.cap));
             RC(dalloc(&t.hit, (size_t)t.cap));
             RC(dalloc(&t.stack, (size_t)t.cap * gp->tail_depth));
@@ -3532,6 +3541,12 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
     // stack_depth the other traversals size their stacks for); k_bvh_bounce's LDS stack is sized
     // by it
     sc.pair_stack_depth = gp->pair_depth > 0 ? std::min(gp->pair_depth, gp->stack_depth) : gp->stack_depth;
+    // the split kernels' LDS stack: all of it, or its first bvh_stack_lds entries and a spill row per
+    // queue slot for the rest
+    sc.stack_lds = gp->split && gp->tune.bvh_stack_lds > 0 ? std::min(gp->tune.bvh_stack_lds, sc.pair_stack_depth)
+                                                           : sc.pair_stack_depth;
+    sc.spill_stride = sc.pair_stack_depth - sc.stack_lds;
+    sc.spill = nullptr;   // allocated with the traversal queue (ensure_frames)
     sc.cam = to_camdev(s->camera);
     sc.shard = sh;
     sc.contrib = gp->d_contrib;

@@ -227,3 +227,33 @@ def test_four_wide_records_bitexact(name, res, depth, lanes, quad, oracle, ptamd
         assert _eq(tr.image(), r.image), (name, quad)
     finally:
         tr.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lds,quad", [(2, 1), (5, 1), (3, 0), (16, 1)])
+@pytest.mark.parametrize("name,res,depth", [("cornell_obj_bnnuy", (96, 96), None),
+                                            ("cornell_obj_khaslana", (64, 64), 12),
+                                            ("cornell_obj_cyrene", (48, 48), None)])
+def test_spilled_stack_bitexact(name, res, depth, lds, quad, oracle, ptamd, monkeypatch):
+    """PT_BVH_STACK_LDS: only the first `lds` traversal stack entries in LDS, deeper ones in a spill
+    row per queue slot -- through the hand-over too (its saved stack is the LDS part; the spilled
+    entries stay in the slot's row) -- bit-exact, with 4-wide records and pairs."""
+    monkeypatch.setenv("PT_BVH_STACK_LDS", str(lds))
+    monkeypatch.setenv("PT_BVH_QUAD", str(quad))
+    a = oracle.load_scene(scene_path(name), res=res, depth=depth)
+    b = ptamd.SceneFile(scene_path(name), res=res, depth=depth)
+    r = oracle.Renderer(a, oracle.options(**BIT))
+    tr = ptamd.PathTracer(b)
+    try:
+        segs = 0
+        for it in range(1, 4):
+            segs += int(np.maximum(r.trace(it), 0).sum())
+        tr.trace_frames(1, 3)
+        assert _eq(tr.image(), r.image), (name, lds, quad)
+        assert tr.stats()["segments_total"] == segs
+        for it in (4, 5):
+            r.trace(it)
+            tr.trace(it, copy_image=True)
+        assert _eq(tr.image(), r.image), (name, lds, quad)
+    finally:
+        tr.free()
