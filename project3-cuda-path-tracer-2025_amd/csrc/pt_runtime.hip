@@ -3275,81 +3275,29 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                     // the top levels, preorder below, as the pairs (PT_BVH_BFS_LEVELS / 2 levels).
                     const bool quad_on = gp->tune.bvh_quad > 0;
                     if (quad_on) {
-                        // children of the record for binary node n (TravChild: leaf -> itself,
-                        // inner -> its two children)
-                        auto kids = [&](int n, pth::TravChild* out) {
-                            int k = 0;
-                            for (int c = 0; c < 2; ++c) {
-                                const pth::TravChild& ch = tt[n].c[c];
-                                if (ch.leaf) out[k++] = ch;
-                                else { out[k++] = tt[ch.ref].c[0]; out[k++] = tt[ch.ref].c[1]; }
-                            }
-                            return k;
-                        };
-                        // the binary nodes that head a record: the root and every inner grandchild
-                        // reached through an inner child, or inner child of ... (every inner kid)
-                        std::vector<int> qnode{0}, qdepth{0};
-                        std::vector<int> qid(P, -1);
-                        qid[0] = 0;
-                        for (size_t h = 0; h < qnode.size(); ++h) {   // breadth-first
-                            pth::TravChild k4[4];
-                            const int nk = kids(qnode[h], k4);
-                            for (int i = 0; i < nk; ++i)
-                                if (!k4[i].leaf) {
-                                    qid[k4[i].ref] = (int)qnode.size();
-                                    qnode.push_back(k4[i].ref);
-                                    qdepth.push_back(qdepth[h] + 1);
-                                }
-                        }
-                        const int Q = (int)qnode.size();
-                        // numbering: breadth-first over the top levels, each subtree below in preorder
-                        const int qlev = std::max(0, gp->tune.bvh_bfs_levels / 2);
-                        std::vector<int> order, num(Q, -1);
-                        std::vector<int> roots;
-                        for (int h = 0; h < Q; ++h) {
-                            if (qdepth[h] < qlev) order.push_back(h);
-                            else if (qdepth[h] == qlev) roots.push_back(h);
-                        }
-                        for (int r : roots) {
-                            std::vector<int> st{r};
-                            while (!st.empty()) {
-                                const int h = st.back();
-                                st.pop_back();
-                                order.push_back(h);
-                                pth::TravChild k4[4];
-                                const int nk = kids(qnode[h], k4);
-                                for (int i = nk - 1; i >= 0; --i)
-                                    if (!k4[i].leaf) st.push_back(qid[k4[i].ref]);
-                            }
-                        }
-                        for (int i = 0; i < (int)order.size(); ++i) num[order[i]] = i;
+                        std::vector<pth::QuadRecord> qr;
+                        int qneed = 0;
+                        pth::build_quad_records(tt, std::max(0, gp->tune.bvh_bfs_levels / 2), qr, qneed);
+                        const int Q = (int)qr.size();
                         quads.assign(8 * (size_t)Q, make_float4(0.f, 0.f, 0.f, 0.f));
-                        std::vector<int> need(Q, 0);   // stack entries below record h (children - 1 per level)
-                        for (int h = Q - 1; h >= 0; --h) {   // children after parents in breadth-first order
-                            pth::TravChild k4[4];
-                            const int nk = kids(qnode[h], k4);
-                            float4* R = &quads[8 * (size_t)num[h]];
-                            int deeper = 0;
+                        for (int q = 0; q < Q; ++q) {
+                            float4* R = &quads[8 * (size_t)q];
+                            float* f[8] = {&R[0].x, &R[1].x, &R[2].x, &R[3].x, &R[4].x, &R[5].x, &R[6].x, &R[7].x};
                             for (int i = 0; i < 4; ++i) {
-                                float* f[8] = {&R[0].x, &R[1].x, &R[2].x, &R[3].x, &R[4].x, &R[5].x, &R[6].x, &R[7].x};
-                                if (i < nk) {
-                                    const pth::TravChild& c = k4[i];
+                                int rf = -1;   // no child
+                                if (i < qr[q].n) {
+                                    const pth::TravChild& c = qr[q].c[i];
                                     for (int a = 0; a < 3; ++a) {
                                         f[a][i] = c.lo[a];
                                         f[3 + a][i] = c.hi[a];
                                     }
-                                    const int rf = c.leaf ? Q + c.ref : num[qid[c.ref]];
-                                    memcpy(&f[6][i], &rf, 4);
+                                    rf = c.leaf ? Q + c.ref : c.ref;
                                     f[7][i] = pack_cull(c.s);
-                                    if (!c.leaf) deeper = std::max(deeper, need[qid[c.ref]]);
-                                } else {
-                                    const int none = -1;
-                                    memcpy(&f[6][i], &none, 4);
                                 }
+                                memcpy(&f[6][i], &rf, 4);
                             }
-                            need[h] = (nk - 1) + deeper;
                         }
-                        quad_stack = need[0] + 1;
+                        quad_stack = qneed + 1;
                         gp->stack_depth = std::max(gp->stack_depth, quad_stack);
                         gp->pair_depth = std::max(gp->pair_depth, quad_stack);   // the push bound covers both
                         if (gp->tune.bvh_tree_info)

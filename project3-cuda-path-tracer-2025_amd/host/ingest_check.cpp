@@ -101,10 +101,39 @@ static int check_scene(const char* path) {
             for (int x : seen) tight_leaves += x == 1;
         }
     }
+    // the 4-wide records: every leaf in exactly one record, every record but the root referenced
+    // exactly once and after its parent... 2..4 children, each child's box the tree's own
+    int quads = -1, quad_ok = -1, quad_need = -1;
+    if (sah) {
+        std::vector<pth::QuadRecord> qr;
+        pth::build_quad_records(tree, 6, qr, quad_need);
+        quads = (int)qr.size();
+        quad_ok = 1;
+        std::vector<int> leaf_seen(s.size(), 0), rec_seen(qr.size(), 0);
+        for (const pth::QuadRecord& r : qr) {
+            if (r.n < 2 || r.n > 4) quad_ok = 0;
+            for (int i = 0; i < r.n; ++i) {
+                const pth::TravChild& c = r.c[i];
+                if (c.leaf) {
+                    if (c.ref < 0 || c.ref >= (int)s.size()) quad_ok = 0;
+                    else leaf_seen[c.ref]++;
+                } else if (c.ref <= 0 || c.ref >= (int)qr.size()) {
+                    quad_ok = 0;
+                } else {
+                    rec_seen[c.ref]++;
+                }
+                for (int a = 0; a < 3; ++a)
+                    if (!(c.lo[a] <= c.hi[a])) quad_ok = 0;
+            }
+        }
+        for (int x : leaf_seen) quad_ok &= x == 1;
+        for (size_t q = 1; q < rec_seen.size(); ++q) quad_ok &= rec_seen[q] == 1;
+        if (!rec_seen.empty()) quad_ok &= rec_seen[0] == 0;
+    }
     std::printf("scene rc=0 geoms=%d materials=%d triangles=%d nodes=%d depth=%d textures=%d bad_tex=%d sah=%d "
-                "sah_orders_equal=%d sah_tight=%d leaves=%zu tight_leaves=%d\n",
+                "sah_orders_equal=%d sah_tight=%d leaves=%zu tight_leaves=%d quads=%d quad_ok=%d quad_stack=%d\n",
                 v.num_geoms, v.num_materials, v.num_triangles, v.num_bvh_nodes, depth, v.num_textures, bad_tex,
-                sah ? height : -1, orders_equal, tight, s.size(), tight_leaves);
+                sah ? height : -1, orders_equal, tight, s.size(), tight_leaves, quads, quad_ok, quad_need);
     pt_scene_free(f);
     return 0;
 }

@@ -220,4 +220,74 @@ bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>&
     return true;
 }
 
+void build_quad_records(const std::vector<TravInner>& tt, int bfs_levels, std::vector<QuadRecord>& out,
+                        int& stack_need) {
+    out.clear();
+    stack_need = 0;
+    if (tt.empty()) return;
+    const int P = (int)tt.size();
+    auto kids = [&](int n, TravChild* k4) {
+        int k = 0;
+        for (int c = 0; c < 2; ++c) {
+            const TravChild& ch = tt[n].c[c];
+            if (ch.leaf) {
+                k4[k++] = ch;
+            } else {
+                k4[k++] = tt[ch.ref].c[0];
+                k4[k++] = tt[ch.ref].c[1];
+            }
+        }
+        return k;
+    };
+    // the binary nodes that head a record, breadth-first: the root and every inner child of a record
+    std::vector<int> head{0}, depth{0}, qid(P, -1);
+    qid[0] = 0;
+    for (size_t h = 0; h < head.size(); ++h) {
+        TravChild k4[4];
+        const int nk = kids(head[h], k4);
+        for (int i = 0; i < nk; ++i)
+            if (!k4[i].leaf) {
+                qid[k4[i].ref] = (int)head.size();
+                head.push_back(k4[i].ref);
+                depth.push_back(depth[h] + 1);
+            }
+    }
+    const int Q = (int)head.size();
+    const int qlev = std::max(0, bfs_levels);
+    std::vector<int> order, num(Q, -1);
+    std::vector<int> roots;
+    for (int h = 0; h < Q; ++h) {
+        if (depth[h] < qlev) order.push_back(h);
+        else if (depth[h] == qlev) roots.push_back(h);
+    }
+    for (int r : roots) {   // each subtree below the breadth-first levels in preorder
+        std::vector<int> st{r};
+        while (!st.empty()) {
+            const int h = st.back();
+            st.pop_back();
+            order.push_back(h);
+            TravChild k4[4];
+            const int nk = kids(head[h], k4);
+            for (int i = nk - 1; i >= 0; --i)
+                if (!k4[i].leaf) st.push_back(qid[k4[i].ref]);
+        }
+    }
+    for (int i = 0; i < (int)order.size(); ++i) num[order[i]] = i;
+    out.assign(Q, QuadRecord{});
+    std::vector<int> need(Q, 0);
+    for (int h = Q - 1; h >= 0; --h) {   // a record's children come after it breadth-first
+        QuadRecord& R = out[num[h]];
+        R.n = kids(head[h], R.c);
+        int deeper = 0;
+        for (int i = 0; i < R.n; ++i)
+            if (!R.c[i].leaf) {
+                const int ch = qid[R.c[i].ref];
+                deeper = std::max(deeper, need[ch]);
+                R.c[i].ref = num[ch];
+            }
+        need[h] = (R.n - 1) + deeper;
+    }
+    stack_need = need[0];
+}
+
 }  // namespace pth

@@ -39,4 +39,17 @@ bool build_sah_tree(const std::vector<float>& leaf_lo, const std::vector<float>&
                     const std::vector<float>& leaf_s, std::vector<TravInner>& out, int& height,
                     int bfs_levels = 1 << 30, int max_height = 1 << 30);
 
+// The 4-wide form of a tree from build_sah_tree: record q holds the children of one binary inner
+// node, an inner child replaced by its own two children (two levels per record: 2 to 4 children).
+// Record 0 is the root's.  Records are numbered breadth-first over the top `bfs_levels` levels and
+// in preorder below; a child is a record (`leaf` false, `ref` its index) or a leaf (`ref` its id).
+// `stack_need`: the most stack entries a depth-first walk that pushes every child but the one it
+// continues with can hold (the sum of children - 1 along a path).
+struct QuadRecord {
+    TravChild c[4];
+    int n;   // children in use
+};
+void build_quad_records(const std::vector<TravInner>& tree, int bfs_levels, std::vector<QuadRecord>& out,
+                        int& stack_need);
+
 }  // namespace pth

@@ -85,6 +85,8 @@ def test_every_repository_scene_and_texture(driver):
         leaves = int(kv["leaves"])
         assert int(kv["sah_tight"]) == 1 + (leaves - 1).bit_length(), (n, res[n])
         assert int(kv["tight_leaves"]) == leaves, (n, res[n])
+        # the 4-wide records hold every leaf once and every record but the root is one child
+        assert kv["quad_ok"] == "1" and 0 < int(kv["quads"]) < leaves, (n, res[n])
     pngs = sorted(glob.glob(os.path.join(REPO, "scenes", "textures", "*.png")) +
                   glob.glob(os.path.join(GOLDEN, "*.png")))
     if pngs:
