@@ -77,6 +77,9 @@ for s in "$@"; do
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- $B --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12 ;;
         occab) ARMS="- PT_BVH_LDS_PAD=5120 PT_BVH_LDS_PAD=11264"
             AB_ROUNDS=2 AB_TAG=occ_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_occ_bunny 900 bash tools/ab_env.sh ;;
+        qorderab) ARMS="${ORDER_ARMS:-- PT_BVH_BFS_LEVELS=0 PT_BVH_BFS_LEVELS=8 PT_BVH_BFS_LEVELS=18}"
+            AB_ROUNDS=2 AB_TAG=qorder_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_qorder_cyrene 900 bash tools/ab_env.sh
+            AB_ROUNDS=2 AB_TAG=qorder_phainon AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_phainon.json --steps 24 --warmup 2" step ab_qorder_phainon 900 bash tools/ab_env.sh ;;
         tailtune) ARMS="${TAIL_ARMS:-- PT_BVH_TAIL_REFILL=8 PT_BVH_TAIL_REFILL=32 PT_BVH_TAIL_TRAV_BLOCKS=160 PT_BVH_TAIL_TRAV_BLOCKS=320}"
             AB_ROUNDS=2 AB_TAG=tailtune_cyrene AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_cyrene.json --steps 24 --warmup 2" step ab_tailtune_cyrene 900 bash tools/ab_env.sh
             AB_ROUNDS=2 AB_TAG=tailtune_bunny AB_ENVS="$ARMS" AB_ARGS="--scene scenes/cornell_obj_bnnuy.json" step ab_tailtune_bunny 900 bash tools/ab_env.sh ;;
