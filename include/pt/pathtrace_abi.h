@@ -293,7 +293,7 @@ int32_t pt_profile_frames(int32_t first_iteration, int32_t count, pt_kernel_time
  * handed-over traversals' kernel, [52..67] handed-over rays by stack depth (8 buckets: count,
  * nodes visited after), [68..71] by a hit found before (no: count, nodes; yes: count, nodes);
  * [72] candidate-table pre-test superset sizes over the live lanes, [73] the sum over waves of
- * each wave's largest superset; n <= 76.  `reset` zeroes them after the read. */
+ * each wave's largest superset, [74] of the size of the union of the wave's supersets; n <= 76.  `reset` zeroes them after the read. */
 int32_t pt_debug_section_counters(uint64_t* out, int32_t n, int32_t reset);
 
 /* Next-frame speculation (pt_set_speculation): frames speculated and frames taken over since

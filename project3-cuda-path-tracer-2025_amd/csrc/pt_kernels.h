@@ -136,6 +136,7 @@ enum { SEC_LOAD, SEC_CULL, SEC_EXACT, SEC_FINISH, SEC_SHADE, SEC_STORE, SEC_N_EX
        SEC_TAIL_BY_HIT = SEC_TAIL_BY_SP + 16,       // ... by "a hit found before": no (count, nodes), yes
        SEC_N_SUP = SEC_TAIL_BY_HIT + 4,             // candidate table: superset sizes over the live lanes
        SEC_N_SUP_WMAX,                              // ... and the sum over waves of the wave's largest
+       SEC_N_SUP_WUNION,                            // ... and of the size of the union of the wave's supersets
        SEC_COUNT };
 constexpr int SEC_SLOTS = 76;
 __device__ unsigned long long g_sections[SEC_SLOTS];
@@ -1421,8 +1422,16 @@ PT_DEV void block_intersect(const SceneDev& sc, const DevGeomHot* lg, bool live,
         PT_HOOK(DUP_CULL, sc, lg, ro, rd, bounded);
     }
     if (TIMING && sc.grid) {   // the per-lane superset loop costs a wave its largest superset
-        int ss = live ? __popcll(grid_superset(sc, ro, rd)) : 0;
+        const uint64_t sup = live ? grid_superset(sc, ro, rd) : 0ull;
+        int ss = __popcll(sup);
         sec_add_lanes(SEC_N_SUP, ss);
+        uint64_t un = sup;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)un, off, 64), hi = __shfl_xor((uint32_t)(un >> 32), off, 64);
+            un |= ((uint64_t)hi << 32) | lo;
+        }
+        sec_add(SEC_N_SUP_WUNION, (uint64_t)__popcll(un));
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) ss = max(ss, __shfl_xor(ss, off, 64));
         sec_add(SEC_N_SUP_WMAX, (uint64_t)ss);

@@ -412,6 +412,7 @@ class PathTracer:
         # candidate-table scenes: superset sizes summed over live lanes, and the waves' maxima
         out["n_sup"] = int(buf[len(self.SECTIONS) + 52])
         out["n_sup_wmax"] = int(buf[len(self.SECTIONS) + 53])
+        out["n_sup_wunion"] = int(buf[len(self.SECTIONS) + 54])
         return out
 
     # ---- single-kernel entry points (tests) ----

@@ -56,7 +56,8 @@ def main():
            "bvh_simt_efficiency": round(c["n_nodes"] / max(1, 64 * c["n_bvh_witers"]), 3),
            "aabb_decision_mismatches": c["n_aabb_mismatch"],
            "superset_per_live_lane": round(c["n_sup"] / lanes, 3),
-           "superset_wave_max_per_wave": round(c["n_sup_wmax"] / max(1, c["n_waves"]), 3), "raw": c}
+           "superset_wave_max_per_wave": round(c["n_sup_wmax"] / max(1, c["n_waves"]), 3),
+           "superset_wave_union_per_wave": round(c["n_sup_wunion"] / max(1, c["n_waves"]), 3), "raw": c}
     # k_bvh_bounce wave steps by active lanes (bins of 4): the steps a wave takes below a given
     # occupancy, and the lane-steps they do (bin centres)
     for key, name in (("bvh_lanes_hist", "bvh_steps_by_active_lanes"), ("tail_lanes_hist", "tail_steps_by_active_lanes")):
