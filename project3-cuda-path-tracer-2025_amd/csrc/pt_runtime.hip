@@ -3278,6 +3278,9 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                         std::vector<pth::QuadRecord> qr;
                         int qneed = 0;
                         pth::build_quad_records(tt, std::max(0, gp->tune.bvh_bfs_levels / 2), qr, qneed);
+                        // the hand-over saves the stack depth in 7 bits (trav_saved_node): deeper
+                        // worst cases (trees far past the height bound) keep the pairs
+                        if (qneed + 1 > 96) qr.clear();
                         const int Q = (int)qr.size();
                         quads.assign(8 * (size_t)Q, make_float4(0.f, 0.f, 0.f, 0.f));
                         for (int q = 0; q < Q; ++q) {
@@ -3297,7 +3300,7 @@ static int32_t init_one(const pt_scene_view* s, pt_options o, int share) {
                                 memcpy(&f[6][i], &rf, 4);
                             }
                         }
-                        quad_stack = qneed + 1;
+                        quad_stack = Q > 0 ? qneed + 1 : 0;
                         gp->stack_depth = std::max(gp->stack_depth, quad_stack);
                         gp->pair_depth = std::max(gp->pair_depth, quad_stack);   // the push bound covers both
                         if (gp->tune.bvh_tree_info)
