@@ -93,13 +93,19 @@ struct SceneDev {
     float grid_lo[3], grid_inv[3]; // cell = floor((o - grid_lo) * grid_inv), GRID_G per axis
 };
 
-// The candidate table's resolution: GRID_G^3 origin cells x 6 faces x GRID_B^2 direction bins
-// (1.5 MB of 64-bit masks at 8 / 8)
+// The candidate table's resolution: GRID_G^3 origin cells x 6 faces x GRID_B^2 direction bins.
+// An entry is the AND of one mask per ratio bin (build_candidate_table), so the table is stored
+// separably (PT_GRID_SEP): 2 GRID_B masks per (cell, face), 6.3 MB at 16 / 16 instead of 50 MB.
+// 16 / 16 against 8 / 8: khaslana superset 5.68 -> 3.60 per ray, 13.8 -> 8.4 at the wave maximum,
+// frame -3 % (DESIGN §4 "Candidate table")
 #ifndef PT_GRID_G
-#define PT_GRID_G 8
+#define PT_GRID_G 16
 #endif
 #ifndef PT_GRID_B
-#define PT_GRID_B 8
+#define PT_GRID_B 16
+#endif
+#ifndef PT_GRID_SEP
+#define PT_GRID_SEP 1
 #endif
 constexpr int GRID_G = PT_GRID_G;
 constexpr int GRID_B = PT_GRID_B;
@@ -933,8 +939,15 @@ PT_DEV uint64_t grid_superset(const SceneDev& sc, f3 ro, f3 rd) {
     const int bv = __builtin_amdgcn_fmed3f(__builtin_truncf((dj * r + 1.f) * HB), 0.f, (float)(GRID_B - 1));
     const int face = (kx ? 0 : (ky ? 2 : 4)) + (dk > 0.f ? 1 : 0);
     const int cell = ((int)fz * GRID_G + (int)fy) * GRID_G + (int)fx;
+#if PT_GRID_SEP
+    // separable table: the (cell, face) row holds the B masks of the first ratio's bins, then the
+    // B masks of the second's; the entry is their AND (two independent loads, 2B words per row)
+    const int e = ok ? (cell * 6 + face) * (2 * GRID_B) : 0;
+    const uint64_t sup = sc.grid[e + (ok ? bu : 0)] & sc.grid[e + (ok ? GRID_B + bv : 0)];
+#else
     const int e = ok ? ((cell * 6 + face) * GRID_B + bu) * GRID_B + bv : 0;
     const uint64_t sup = sc.grid[e];
+#endif
     return ok ? sup : sc.grid_all;
 }
 template <bool TIMING = false, bool NEAR_FIRST = false>

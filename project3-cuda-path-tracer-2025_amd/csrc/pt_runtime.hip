@@ -2077,7 +2077,7 @@ bool build_candidate_table(const std::vector<DevCull>& culls, int ng, const pt_v
     }
     const double cm = 1e-6 * ext, bin_eps = 1e-5;
     const int G = GRID_G, B = GRID_B;
-    table.assign((size_t)G * G * G * 6 * B * B, 0ull);
+    table.assign((size_t)G * G * G * 6 * (PT_GRID_SEP ? 2 * B : B * B), 0ull);
     std::vector<double> ta(ng), tb(ng);
     std::vector<unsigned long long> mi(B), mj(B);
     for (int cz = 0; cz < G; ++cz)
@@ -2119,6 +2119,14 @@ bool build_candidate_table(const std::vector<DevCull>& culls, int ng, const pt_v
                             }
                             m[b] = bits;
                         }
+                    }
+                    if (PT_GRID_SEP) {   // the device ANDs the two bins' masks
+                        unsigned long long* row = &table[((size_t)cell * 6 + face) * 2 * B];
+                        for (int b = 0; b < B; ++b) {
+                            row[b] = mi[b];
+                            row[B + b] = mj[b];
+                        }
+                        continue;
                     }
                     unsigned long long* row = &table[((size_t)cell * 6 + face) * B * B];
                     for (int bu = 0; bu < B; ++bu)

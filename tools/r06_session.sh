@@ -21,6 +21,22 @@ for s in "$@"; do
     case $s in
         new) step pytest_new 500 $PYT tests/test_multi_device.py tests/test_dropin.py -m gpu ;;
         spec) step pytest_spec 300 $PYT tests/test_speculation.py -m gpu ;;
+        gridres)   # candidate-table resolution: superset sizes per build, then khaslana A/B
+            for v in ${GRID_VARS:-s16b16 s24b24}; do
+                PTAMD_LIB=$PWD/project3-cuda-path-tracer-2025_amd/build/ab/$v.so PT_SECTIONS_SKIP_CAMERA=1 \
+                    step sec_kh_$v 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_kh_$v.json
+            done
+            PT_SECTIONS_SKIP_CAMERA=1 step sec_kh_base 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_kh_base.json
+            L=project3-cuda-path-tracer-2025_amd/build
+            AB_ROUNDS=2 AB_LIBS="$L/libptamd.so ${GRID_AB:-$L/ab/g16b16.so $L/ab/s16b16.so $L/ab/s16b32.so $L/ab/s24b24.so}" AB_TAG=gridres_khaslana \
+                AB_ARGS="--steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_gridres_khaslana 900 bash tools/ab_libs.sh ;;
+        gridab)   # the old 8 / 8 full table (build/ab/old.so) against the product build
+            L=project3-cuda-path-tracer-2025_amd/build
+            for sc in cornell_obj_khaslana cornell_obj_cyrene cornell_obj_phainon; do
+                X=""; [ $sc = cornell_obj_khaslana ] && X="--res 1600x1600 --depth 12"
+                AB_ROUNDS=3 AB_LIBS="$L/ab/old.so $L/libptamd.so" AB_TAG=grid_$sc \
+                    AB_ARGS="--steps 24 --warmup 2 --scene scenes/$sc.json $X" step ab_grid_$sc 600 bash tools/ab_libs.sh
+            done ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
         meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
         mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
