@@ -32,9 +32,9 @@ for s in "$@"; do
                 AB_ARGS="--steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_gridres_khaslana 900 bash tools/ab_libs.sh ;;
         gridab)   # the old 8 / 8 full table (build/ab/old.so) against the product build
             L=project3-cuda-path-tracer-2025_amd/build
-            for sc in cornell_obj_khaslana cornell_obj_cyrene cornell_obj_phainon; do
+            for sc in ${GRID_SCENES:-cornell_obj_khaslana cornell_obj_cyrene cornell_obj_phainon}; do
                 X=""; [ $sc = cornell_obj_khaslana ] && X="--res 1600x1600 --depth 12"
-                AB_ROUNDS=3 AB_LIBS="$L/ab/old.so $L/libptamd.so" AB_TAG=grid_$sc \
+                AB_ROUNDS=3 AB_LIBS="$L/ab/${GRID_OLD:-old}.so $L/libptamd.so" AB_TAG=grid_$sc \
                     AB_ARGS="--steps 24 --warmup 2 --scene scenes/$sc.json $X" step ab_grid_$sc 600 bash tools/ab_libs.sh
             done ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
