@@ -2054,7 +2054,10 @@ int bvh_height(const pt_bvh_node* nodes, int n) {
 // condition.  Every exact hit point lies in that box (the pre-test's premise, cull_geom), so a geom
 // outside the entry cannot be hit.  The cells are grown by far more than the device's float
 // cell computation can be off, the bins likewise for its rcp-based ratio, the boxes by 1e-6 of
-// the scene.  Returns false (no table) for scenes whose geom boxes are not finite.
+// the scene.  The two ratio axes are bounded independently, so an entry is the AND of one mask
+// per bin of each: with PT_GRID_SEP the table holds those 2 GRID_B masks per (cell, face) and the
+// device ANDs them (the same entries in 2 / GRID_B of the words).  Returns false (no table) for
+// scenes whose geom boxes are not finite.
 bool build_candidate_table(const std::vector<DevCull>& culls, int ng, const pt_vec3& cam,
                            std::vector<unsigned long long>& table, float lo_out[3], float inv_out[3]) {
     double lo[3] = {cam.x, cam.y, cam.z}, hi[3] = {cam.x, cam.y, cam.z};
