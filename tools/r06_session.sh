@@ -42,6 +42,11 @@ for s in "$@"; do
             step prof_c5_khaslana 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_khaslana -o run --output-format csv -- python bench.py --no-cpu-baseline --no-configs --no-api --no-spread --steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
             PMC_TAG=khtr_ PMC_STEPS=8 PMC_WARMUP=2 PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_khtr 400 bash tools/pmc.sh --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
             PT_SECTIONS_SKIP_CAMERA=1 step sec_khaslana 300 python -u tools/section_times.py --scene cornell_obj_khaslana --res 1600x1600 --depth 12 --variant 190 --frames 8 --out gpurun_out/sec_khaslana.json ;;
+        cyrprof)   # the 262k stand-in's kernel stats, PMC traffic and sections at the current build
+            rm -rf gpurun_out/prof_m262k_cyrene gpurun_out/pmc/cyr_p*
+            step prof_m262k_cyrene 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_m262k_cyrene -o run --output-format csv -- python bench.py --no-cpu-baseline --no-configs --no-api --no-spread --steps 24 --warmup 2 --scene scenes/cornell_obj_cyrene.json
+            PMC_TAG=cyr_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_cyr 400 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json
+            step sec_cyrene 300 python -u tools/section_times.py --scene cornell_obj_cyrene --variant 190 --frames 16 --out gpurun_out/sec_cyrene.json ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
         meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
         mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
