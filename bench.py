@@ -427,7 +427,12 @@ def sub_config(ptamd, cfg):
                                               "c5_khaslana" if "khaslana" in scene_name and res == (1600, 1600)
                                               and depth == 12 else
                                               "staged_c2" if pipeline == "staged" and "glass" in scene_name and sort
+                                              else "c2_glass" if "glass" in scene_name and sort
+                                              else "c2_glass_sortoff" if "glass" in scene_name
                                               else "m262k_cyrene" if "cyrene" in scene_name and not opts
+                                              else "m262k_cyrene_nodes" if "cyrene" in scene_name
+                                              else "m1m_phainon" if "phainon" in scene_name and not opts
+                                              else "m1m_phainon_nodes" if "phainon" in scene_name
                                               else None)),
            "kernels": kernels_digest(prof, None)}
     if "obj" in scene_name:

@@ -47,6 +47,13 @@ for s in "$@"; do
             step prof_m262k_cyrene 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_m262k_cyrene -o run --output-format csv -- python bench.py --no-cpu-baseline --no-configs --no-api --no-spread --steps 24 --warmup 2 --scene scenes/cornell_obj_cyrene.json
             PMC_TAG=cyr_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_cyr 400 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json
             step sec_cyrene 300 python -u tools/section_times.py --scene cornell_obj_cyrene --variant 190 --frames 16 --out gpurun_out/sec_cyrene.json ;;
+        cfgpmc)   # PMC traffic of the sub-records that had none (bench.py traffic_file names)
+            T="FETCH_SIZE;WRITE_SIZE"
+            PMC_TAG=c2g_ PMC_SETS="$T" step pmc_c2g 300 bash tools/pmc.sh --scene scenes/cornell_glass_test.json --sort
+            PMC_TAG=c2o_ PMC_SETS="$T" step pmc_c2o 300 bash tools/pmc.sh --scene scenes/cornell_glass_test.json
+            PMC_TAG=phn_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="$T" step pmc_phn 400 bash tools/pmc.sh --scene scenes/cornell_obj_phainon.json
+            PMC_TAG=cyrn_ PMC_STEPS=8 PMC_WARMUP=1 PMC_SETS="$T" step pmc_cyrn 400 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json --variant 250
+            PMC_TAG=phnn_ PMC_STEPS=8 PMC_WARMUP=1 PMC_SETS="$T" step pmc_phnn 400 bash tools/pmc.sh --scene scenes/cornell_obj_phainon.json --variant 250 ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
         meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
         mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
