@@ -390,6 +390,24 @@ def kernels_digest(prof, spread):
     return d
 
 
+def traffic_tag(cfg):
+    """The committed PMC digest (profiles/rNN_traffic_<tag>.json) of a SUB_CONFIGS entry: PMC passes
+    of the same bench command (tools/r06_session.sh cfgpmc / khprof / cyrprof)."""
+    _, scene_name, res, depth, sort, pipeline = cfg[:6]
+    opts = cfg[8] if len(cfg) > 8 else {}
+    if "bnnuy" in scene_name and res is None:
+        return "c4_bunny"
+    if "khaslana" in scene_name and res == (1600, 1600) and depth == 12:
+        return "c5_khaslana"
+    if "glass" in scene_name:
+        return ("staged_c2" if pipeline == "staged" else "c2_glass") if sort else "c2_glass_sortoff"
+    if "cyrene" in scene_name:
+        return "m262k_cyrene_nodes" if opts else "m262k_cyrene"
+    if "phainon" in scene_name:
+        return "m1m_phainon_nodes" if opts else "m1m_phainon"
+    return None
+
+
 def sub_config(ptamd, cfg):
     """One BASELINE config on this GPU: warmup, K timed frames (pass graphs), eager profiled
     replay for its roofline.  Same timing rules as the headline."""
@@ -423,17 +441,7 @@ def sub_config(ptamd, cfg):
            "segments_per_frame": round(st["segments_total"] / steps, 1), "frames_per_pass": st["frames_per_pass"],
            "data": "synthetic stand-in meshes (reference OBJs absent)" if "obj" in scene_name else "reference scene",
            "roofline": roofline(prof, st_prof, pipeline, steps, d, False,
-                                traffic_file=("c4_bunny" if "bnnuy" in scene_name and res is None else
-                                              "c5_khaslana" if "khaslana" in scene_name and res == (1600, 1600)
-                                              and depth == 12 else
-                                              "staged_c2" if pipeline == "staged" and "glass" in scene_name and sort
-                                              else "c2_glass" if "glass" in scene_name and sort
-                                              else "c2_glass_sortoff" if "glass" in scene_name
-                                              else "m262k_cyrene" if "cyrene" in scene_name and not opts
-                                              else "m262k_cyrene_nodes" if "cyrene" in scene_name
-                                              else "m1m_phainon" if "phainon" in scene_name and not opts
-                                              else "m1m_phainon_nodes" if "phainon" in scene_name
-                                              else None)),
+                                traffic_file=traffic_tag(cfg)),
            "kernels": kernels_digest(prof, None)}
     if "obj" in scene_name:
         out["triangles"] = len(sc.triangles)

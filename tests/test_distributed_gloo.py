@@ -138,3 +138,17 @@ def test_bench_refuses_more_rccl_ranks_than_gpus():
     p = subprocess.run([sys.executable, os.path.join(os.path.dirname(PKG), "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "RCCL ranks" in p.stderr, p.stderr[-400:]
+
+
+def test_bench_sub_records_have_traffic_digests():
+    """Every bench `configs` sub-record names a committed PMC digest (profiles/rNN_traffic_<tag>.json)
+    with HBM bytes per frame for the kernels its roofline covers, so no record's `traffic` is null."""
+    sys.path.insert(0, os.path.dirname(PKG))
+    import bench
+    for cfg in bench.SUB_CONFIGS:
+        tag = bench.traffic_tag(cfg)
+        assert tag, cfg[0]
+        d = bench._pmc_digest(tag)
+        assert d, (cfg[0], tag)
+        k = "k_compact_scatter" if cfg[5] == "staged" else "k_bounce"
+        assert d.get(k, {}).get("hbm_bytes_per_frame", 0) > 0, (cfg[0], tag)
