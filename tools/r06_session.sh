@@ -54,6 +54,13 @@ for s in "$@"; do
             PMC_TAG=phn_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="$T" step pmc_phn 400 bash tools/pmc.sh --scene scenes/cornell_obj_phainon.json
             PMC_TAG=cyrn_ PMC_STEPS=8 PMC_WARMUP=1 PMC_SETS="$T" step pmc_cyrn 400 bash tools/pmc.sh --scene scenes/cornell_obj_cyrene.json --variant 250
             PMC_TAG=phnn_ PMC_STEPS=8 PMC_WARMUP=1 PMC_SETS="$T" step pmc_phnn 400 bash tools/pmc.sh --scene scenes/cornell_obj_phainon.json --variant 250 ;;
+        khvar)   # khaslana traffic with a variant library (KH_LIB), then the A/B against the product
+            PTAMD_LIB=$PWD/$KH_LIB PMC_TAG=khv_ PMC_STEPS=8 PMC_WARMUP=2 PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_khv 400 bash tools/pmc.sh --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12
+            L=project3-cuda-path-tracer-2025_amd/build
+            AB_ROUNDS=3 AB_LIBS="$L/libptamd.so $KH_LIB" AB_TAG=khvar \
+                AB_ARGS="--steps 32 --warmup 2 --scene scenes/cornell_obj_khaslana.json --res 1600x1600 --depth 12" step ab_khvar 600 bash tools/ab_libs.sh ;;
+        phnpmc) rm -rf gpurun_out/pmc/phn_p*
+            PMC_TAG=phn_ PMC_STEPS=16 PMC_WARMUP=2 PMC_SETS="FETCH_SIZE;WRITE_SIZE" step pmc_phn 400 bash tools/pmc.sh --scene scenes/cornell_obj_phainon.json ;;
         glibc) step pytest_glibc 300 $PYT tests/test_gpu_parity.py -m gpu -k statistical ;;
         meshlib) PTAMD_LIB=$PWD/${MESH_LIB} step pytest_meshlib 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py tests/test_speculation.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections or speculated" ;;
         mesh) step pytest_mesh 600 $PYT tests/test_gpu_parity.py tests/test_ref_pins.py -m gpu -k "bnnuy or khaslana or bvh or mesh or candidate or config5 or intersections" ;;
